@@ -1,0 +1,195 @@
+"""bench.py - device-resident dissection throughput on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): 16,777,216 synthetic 64 B
+Eth/IPv4/UDP frames per GPU, resident in HBM; one step = one pass of the
+dissector chain kernel over the batch (records + ext + per-protocol counters)
+plus, for N > 1 GPUs, the RCCL all-reduce of the counter vector.
+--config imix / ipv6x select C3 / C4 instead.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU, weak scaling: every rank walks its
+own 16M-packet shard).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "netsniff-ng_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import nsd  # noqa: E402
+import nsd_testlib as T  # noqa: E402  (input generators; oracle only in cpu_baseline)
+
+CONFIGS = {
+    "udp64": dict(cfg=T.SYN_UDP64, name="C2: 16M x 64 B Eth/IPv4/UDP"),
+    "imix": dict(cfg=T.SYN_IMIX, name="C3: 16M IMIX 64/576/1500 Eth/[VLAN]/IPv4/{TCP,UDP,ICMP}"),
+    "ipv6x": dict(cfg=T.SYN_IPV6X, name="C4: 16M IPv6 + 0..6 extension headers"),
+}
+HBM_PEAK_GBS = 8000.0      # MI355X spec (MI355X_MICROARCH.md)
+REC_B, DESC_B = 16, 8
+
+
+def wsum_for(cfg_key, n, lo):
+    """Sum of algorithmic read bytes W over the shard (DESIGN.md "Roofline").
+    C2: every frame is 64 B, W = caplen.  C3/C4: committed per-config sums
+    (tests/golden/wsum.json, made by tests/golden/make_golden.py from the CPU
+    restatement) for the standard 16M shard at lo = 0, else None."""
+    if cfg_key == "udp64":
+        return 64 * n
+    path = os.path.join(ROOT, "tests", "golden", "wsum.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            table = json.load(f)
+        key = f"{cfg_key}:{lo}:{n}"
+        if key in table:
+            return int(table[key])
+    return None
+
+
+def cpu_baseline(cfg, n_sample, threads):
+    """CPU restatement (oracle, "port") timed on this host: fields-only walk
+    with `threads` threads over a bounded sample."""
+    frames, desc = T.make_batch(cfg, n_sample, lo=0)
+    lib = T.oracle()
+    counters = np.zeros(64, dtype=np.uint64)
+    rec = np.zeros(n_sample, dtype=T.REC_DTYPE)
+    t0 = time.perf_counter()
+    lib.nsor_dissect_batch_mt(frames.ctypes.data, desc.ctypes.data, n_sample, 1, T.PRINT_NORM,
+                              rec.ctypes.data, counters.ctypes.data, threads)
+    dt = time.perf_counter() - t0
+    return n_sample / dt / 1e6, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="udp64", choices=sorted(CONFIGS))
+    ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
+    ap.add_argument("--mode", type=int, default=nsd.PRINT_NORM)
+    ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 21)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    c = CONFIGS[args.config]
+    n = args.packets
+    lo = rank * n
+    frames_np, desc_np = T.make_batch(c["cfg"], n, lo=lo, threads=16)
+    frames = torch.from_numpy(frames_np).to(dev)
+    desc = torch.from_numpy(desc_np.view(np.int64)).to(dev)
+    frame_bytes = int(T.desc_caplen(desc_np).sum())
+    del frames_np
+    ext_cap = n if args.config == "ipv6x" else max(n // 64, 4096)
+    rec = torch.empty(n * REC_B, dtype=torch.uint8, device=dev)
+    ext = torch.empty(ext_cap * nsd.EXT_BYTES, dtype=torch.uint8, device=dev)
+    ext_count = torch.zeros(1, dtype=torch.int32, device=dev)
+    counters = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device=dev)
+
+    def step(ev=None):
+        ext_count.zero_()
+        counters.zero_()
+        if ev is not None:
+            ev[0].record()
+        nsd.dissect_device(frames, desc, mode=args.mode, rec=rec, ext=ext, ext_count=ext_count,
+                           counters=counters, grid=args.grid)
+        if ev is not None:
+            ev[1].record()
+        if dist is not None:
+            dist.all_reduce(counters)   # RCCL over xGMI: per-protocol counters
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    cnt = counters.cpu().numpy().view(np.uint64)
+    total_pkts = n * world
+    assert int(cnt[nsd.CNT_PKTS]) == total_pkts, "counter check failed"
+    ms_per_step = elapsed / args.steps * 1e3
+    mpps = total_pkts * args.steps / elapsed / 1e6
+
+    wsum = wsum_for(args.config, n, lo)
+    roofline = None
+    if wsum is not None:
+        read_b = DESC_B * n + wsum
+        total_b = read_b + REC_B * n
+        achieved = total_b / (kern_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": None,
+                    "read_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "bytes_per_pkt": {"read": round(read_b / n, 2), "write": REC_B},
+                    "kernel_ms": round(kern_ms, 4)}
+        prof = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(prof):
+            with open(prof) as f:
+                roofline["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = min(os.cpu_count() or 1, 16)
+        v1, d1 = cpu_baseline(c["cfg"], args.cpu_sample // 4, 1)
+        vN, dN = cpu_baseline(c["cfg"], args.cpu_sample, threads)
+        cpu = {"value": round(vN, 3), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+               "sample": f"{args.cpu_sample} packets of {args.config} (fields-only restatement walk,"
+                         f" {threads} threads, {dN:.1f} s); 1 thread: {v1:.3f} Mpkt/s"}
+
+    if rank == 0:
+        out = {
+            "metric": "Mpkt/s device-resident dissect (bit-exact fields vs ref)",
+            "value": round(mpps, 2), "unit": "Mpkt/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded splitmix64 generators, tools/nsd_synth.c)",
+            "config": {"workload": c["name"], "packets_per_gpu": n, "frame_bytes_per_gpu": frame_bytes,
+                       "mode": ["PRINT_NORM", "PRINT_LESS", "PRINT_HEX", "PRINT_ASCII",
+                                "PRINT_HEX_ASCII", "PRINT_NONE"][args.mode],
+                       "parallelism": f"dp{world}"},
+            "gbps_frames": round(frame_bytes * world * args.steps / elapsed / 1e9, 1),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,226 @@
+/*
+ * netsniff_dissect.h - C ABI of the MI355X-native netsniff-ng dissection path.
+ *
+ * Drop-in boundary for netsniff-ng's per-packet dissector chain
+ * (reference: dissector.h:118-122, dissector.c:22-138, dissector_eth.c:17-86,
+ * proto.h:18-26, pkt_buff.h:15-110).  Two surfaces:
+ *
+ *   1. The reference surface, same names / argument meaning / behaviour:
+ *        dissector_init_all        <- dissector.h:118 / dissector.c:124-130
+ *        dissector_entry_point     <- dissector.h:119 / dissector.c:64-122
+ *        dissector_cleanup_all     <- dissector.h:121 / dissector.c:132-138
+ *        dissector_set_print_type  <- dissector.h:122 / dissector.c:22-41
+ *      The per-packet entry point runs the packet through the HIP kernel
+ *      (batch of one) and renders the record with the host formatter.
+ *
+ *   2. The batch extension (new): a packed batch of frames is
+ *      walked by hand-written CDNA4 kernels, one lane per packet, producing
+ *      a 16-byte chain record per packet, an overflow table for deep chains
+ *      and a per-protocol counter vector.
+ *
+ * Plain C types only (no torch / HIP types); a stream is passed as void *
+ * (a hipStream_t, NULL = the null stream).
+ */
+#ifndef NETSNIFF_DISSECT_H
+#define NETSNIFF_DISSECT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- print modes (dissector.h:22-27) ---------------------------------- */
+#define PRINT_NORM      0
+#define PRINT_LESS      1
+#define PRINT_HEX       2
+#define PRINT_ASCII     3
+#define PRINT_HEX_ASCII 4
+#define PRINT_NONE      5
+
+/* ---- link types the entry point switches on (linktype.h, dissector.c:77-104) */
+#define NSD_LINKTYPE_EN10MB            1
+#define NSD_LINKTYPE_IEEE802_11        105
+#define NSD_LINKTYPE_LINUX_SLL         113
+#define NSD_LINKTYPE_IEEE802_11_RADIOTAP 127
+#define NSD_LINKTYPE_NETLINK           253
+
+/* ---- protocol-chain IDs: one per ops object (protos.h:6-31) -------------
+ * Identity is the ops struct, not the hash key: none_ops and icmpv4_ops share
+ * key 0x01, ethernet_ops and ipv6_hop_by_hop_ops share key 0. */
+enum nsd_ops_id {
+	NSD_OPS_INVALID        = 0,
+	NSD_OPS_ETHERNET       = 1,   /* proto_ethernet.c:99      key 0      */
+	NSD_OPS_VLAN           = 2,   /* proto_vlan.c:57          0x8100     */
+	NSD_OPS_QINQ           = 3,   /* proto_vlan_q_in_q.c:58   0x88a8     */
+	NSD_OPS_MPLS_UC        = 4,   /* proto_mpls_unicast.c:104  0x8847     */
+	NSD_OPS_ARP            = 5,   /* proto_arp.c:198          0x0806     */
+	NSD_OPS_LLDP           = 6,   /* proto_lldp.c:490         0x88cc     */
+	NSD_OPS_IPV4           = 7,   /* proto_ipv4.c:206         0x0800     */
+	NSD_OPS_IPV6           = 8,   /* proto_ipv6.c:115         0x86DD     */
+	NSD_OPS_IPV6_IN_IPV4   = 9,   /* proto_ipv6_in_ipv4.c:20  41         */
+	NSD_OPS_ICMPV4         = 10,  /* proto_icmpv4.c:63        1          */
+	NSD_OPS_ICMPV6         = 11,  /* proto_icmpv6.c:1701      58         */
+	NSD_OPS_IGMP           = 12,  /* proto_igmp.c:556         2          */
+	NSD_OPS_IP_AUTH        = 13,  /* proto_ip_authentication_hdr.c:90  51 */
+	NSD_OPS_IP_ESP         = 14,  /* proto_ip_esp.c:48        50         */
+	NSD_OPS_IPV6_DEST_OPTS = 15,  /* proto_ipv6_dest_opts.c:97  60       */
+	NSD_OPS_IPV6_FRAGM     = 16,  /* proto_ipv6_fragm.c:65    44         */
+	NSD_OPS_IPV6_HOP_BY_HOP= 17,  /* proto_ipv6_hop_by_hop.c:96  0       */
+	NSD_OPS_IPV6_MOBILITY  = 18,  /* proto_ipv6_mobility_hdr.c:311 135   */
+	NSD_OPS_IPV6_NO_NEXT   = 19,  /* proto_ipv6_no_nxt_hdr.c:36  59      */
+	NSD_OPS_IPV6_ROUTING   = 20,  /* proto_ipv6_routing.c:158 43         */
+	NSD_OPS_TCP            = 21,  /* proto_tcp.c:153          6          */
+	NSD_OPS_UDP            = 22,  /* proto_udp.c:85           17         */
+	NSD_OPS_DCCP           = 23,  /* proto_dccp.c:150         33         */
+	NSD_OPS_NONE           = 24,  /* proto_none.c:79          exit op    */
+	NSD_OPS_SLL            = 25,  /* dissector_sll.c:84       (host)     */
+	NSD_OPS_IEEE80211      = 26,  /* proto_80211_mac_hdr.c:3269 (host)     */
+	NSD_OPS_NLMSG          = 27,  /* proto_nlmsg.c:1058       (host)     */
+	NSD_OPS_COUNT          = 28
+};
+
+/* ---- batch input --------------------------------------------------------
+ * Frames live in one byte buffer; packet i is described by one 64-bit word:
+ * bits 0..39 = byte offset of the frame in the buffer (any alignment),
+ * bits 40..63 = caplen (tp_snaplen).  caplen must be <= NSD_MAX_CAPLEN.
+ * The buffer must stay readable for NSD_FRAME_PAD bytes past its last frame
+ * (the kernel loads whole 16-byte chunks and masks bytes >= caplen to zero).
+ * Bytes at offsets >= caplen read as zero: this is the parity domain's
+ * definition of out-of-frame bytes (SURVEY §8a "Parity domain"). */
+typedef uint64_t nsd_desc_t;
+#define NSD_DESC(off, caplen)   ((((uint64_t)(caplen)) << 40) | ((uint64_t)(off) & 0xFFFFFFFFFFull))
+#define NSD_DESC_OFF(d)         ((uint64_t)(d) & 0xFFFFFFFFFFull)
+#define NSD_DESC_CAPLEN(d)      ((uint32_t)((uint64_t)(d) >> 40))
+#define NSD_MAX_CAPLEN          65535u
+#define NSD_FRAME_PAD           64u
+
+/* ---- per-packet chain record (16 bytes, written by the device) ----------
+ * chain   : ops ID of layer k in bits [5k, 5k+5), k = 0..5.
+ * data_off: final pkt->data; the exit op (none_ops) covers [data_off, tail_off).
+ * tail_off: final pkt->tail (caplen unless the IPv4 trim, proto_ipv4.c:174, cut it).
+ * ip_csum : IPv4 header checksum as the reference computes it
+ *           (calc_csum over ihl*4 bytes, proto_ipv4.c:51); 0 means "ok".
+ *           Only computed in PRINT_NORM; 0 otherwise.
+ * nflags  : bits 0..2 = number of layers run (0..6), 7 = NSD_N_EXT (the full
+ *           chain is in the ext table, slot = off2[0..3] little-endian u32);
+ *           bits 3..7 = NSD_F_* flags.
+ * off2[k-1]: start offset of layer k divided by 2, k = 1..5 (layer 0 starts
+ *           at 0). Every layer start is even, and offsets > 510
+ *           force the ext form.
+ */
+typedef struct nsd_rec {
+	uint32_t chain;
+	uint16_t data_off;
+	uint16_t tail_off;
+	uint16_t ip_csum;
+	uint8_t  nflags;
+	uint8_t  off2[5];
+} nsd_rec;
+
+#define NSD_REC_MAX_LAYERS   6
+#define NSD_N_EXT            7
+#define NSD_F_ICMP_BAD       0x08  /* ICMPv4 checksum nonzero: "bogus (!)" (proto_icmpv4.c:74-81) */
+#define NSD_F_HOST           0x10  /* last layer's body is rendered by the host (ICMPv6 130-154,
+                                      ARP, LLDP, IGMP, DCCP, non-Ethernet link types) */
+#define NSD_F_OVERFLOW       0x20  /* chain longer than NSD_EXT_MAX_LAYERS or ext table full:
+                                      record holds the first layers only */
+
+#define NSD_REC_NLAYERS(r)   ((r)->nflags & 7u)
+#define NSD_REC_ID(r, k)     (((r)->chain >> (5u * (k))) & 31u)
+
+/* Overflow ("ext") record for chains longer than 6 layers or with a layer
+ * starting past byte 510.  Slots are taken with a wave-aggregated atomic. */
+#define NSD_EXT_MAX_LAYERS   64
+typedef struct nsd_ext {
+	uint32_t pkt;                      /* packet index within the batch */
+	uint16_t nlayers;
+	uint16_t rsvd;
+	uint8_t  id[NSD_EXT_MAX_LAYERS];
+	uint16_t off[NSD_EXT_MAX_LAYERS];  /* start offset of each layer */
+} nsd_ext;                             /* 200 bytes */
+
+/* ---- per-protocol counter vector (u64, summed over the batch) ----------- */
+enum nsd_counter {
+	NSD_CNT_OPS       = 0,   /* [0, NSD_OPS_COUNT): layer instances per ops ID */
+	NSD_CNT_PKTS      = 32,  /* packets walked */
+	NSD_CNT_BYTES     = 33,  /* sum of caplen */
+	NSD_CNT_IP_BAD    = 34,  /* IPv4 header checksum bogus (PRINT_NORM) */
+	NSD_CNT_ICMP_BAD  = 35,  /* ICMPv4 checksum bogus (PRINT_NORM) */
+	NSD_CNT_HOST      = 36,  /* records flagged NSD_F_HOST */
+	NSD_CNT_EXT       = 37,  /* records using the ext table */
+	NSD_CNT_OVERFLOW  = 38,  /* records flagged NSD_F_OVERFLOW */
+	NSD_CNT_TRIM      = 39,  /* IPv4 tail trims (tail_off < caplen) */
+	NSD_NCOUNTERS     = 64
+};
+
+/* ---- status codes ------------------------------------------------------ */
+#define NSD_OK               0
+#define NSD_ERR_ARG         -1
+#define NSD_ERR_HIP         -2
+#define NSD_ERR_CAPLEN      -3
+#define NSD_ERR_NOMEM       -4
+#define NSD_ERR_FORMAT      -5
+
+/* ---- reference surface (dissector.h:118-122) ---------------------------- */
+struct sockaddr_ll;
+void dissector_init_all(int fnttype);
+void dissector_entry_point(uint8_t *packet, size_t len, int linktype, int mode,
+			   struct sockaddr_ll *sll);
+void dissector_cleanup_all(void);
+int  dissector_set_print_type(void *ptr, int type);
+
+/* ---- batch extension ---------------------------------------------------- */
+
+/* Device-resident walk: every pointer is device memory, the call only
+ * enqueues work on `stream` (no host synchronisation, graph-capturable).
+ * `d_counters` (NSD_NCOUNTERS u64) is accumulated into, not overwritten;
+ * `d_ext_count` (one u32) likewise.  `mode` selects the parse semantics
+ * (print_full vs print_less chains differ, SURVEY §8a quirk 7 / mobility).
+ * Returns NSD_OK or an error without launching. */
+int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
+		       int linktype, int mode,
+		       nsd_rec *d_rec, nsd_ext *d_ext, uint32_t ext_cap,
+		       uint32_t *d_ext_count, uint64_t *d_counters, void *stream);
+
+/* Host-memory batch: stages frames/descriptors to HBM, runs
+ * nsd_dissect_device, copies records/ext/counters back.  Synchronous.
+ * `counters` may be NULL; `ext` may be NULL when ext_cap == 0. */
+int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
+			  const nsd_desc_t *desc, uint32_t n, int linktype, int mode,
+			  nsd_rec *rec, nsd_ext *ext, uint32_t ext_cap,
+			  uint32_t *ext_count, uint64_t *counters);
+
+/* Host formatter: renders one record + its raw frame bytes into the exact
+ * text the reference dissector chain prints (unwrapped tprintf stream, i.e.
+ * what dissector_entry_point hands to tprintf for this packet).
+ * `ext_table` is the ext array the record's slot refers to (may be NULL if
+ * the record has no ext slot).  Writes at most `cap` bytes (NUL-terminated
+ * when room), returns the full text length, or a negative NSD_ERR_*. */
+long nsd_format_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+		       const nsd_rec *rec, const nsd_ext *ext_table,
+		       char *out, size_t cap);
+
+/* Name tables (lookup.c:33-95): load udp.conf / tcp.conf / ether.conf /
+ * oui.conf from `dir` (the reference's ETCDIRE_STRING).  NULL or a missing
+ * file leaves that table empty (names not printed, vendor "Unknown").
+ * Returns the number of tables loaded. */
+int nsd_lookup_init(const char *dir);
+void nsd_lookup_cleanup(void);
+
+/* tprintf wrap emulation (tprintf.c:65-103): rewrap an unwrapped text
+ * stream for a terminal `cols` wide, carrying the line counter in *state
+ * (start with 0).  Returns bytes written to out (cap must be >= 2*len+16). */
+long nsd_tprintf_wrap(const char *in, size_t len, int cols, long *state,
+		      char *out, size_t cap);
+
+/* Library / device info. */
+const char *nsd_version(void);
+int nsd_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NETSNIFF_DISSECT_H */

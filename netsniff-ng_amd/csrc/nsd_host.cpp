@@ -1,0 +1,364 @@
+// nsd_host.cpp - C ABI of the dissector path (include/netsniff_dissect.h):
+// the reference surface (dissector_init_all / dissector_entry_point /
+// dissector_cleanup_all / dissector_set_print_type, dissector.c:22-138) and
+// the batch extension (nsd_dissect_device / dissector_entry_batch).
+//
+// Every dissection goes through the HIP kernel (nsd_kernels.hip); there is no
+// CPU walk in this library.  If no GPU is usable the calls fail loudly
+// (NSD_ERR_HIP, and dissector_entry_point aborts like the reference's panic()).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/ioctl.h>
+#include <unistd.h>
+
+#include <mutex>
+#include <string>
+
+#include "../../include/netsniff_dissect.h"
+
+extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
+				  int start_id, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+				  int grid, hipStream_t stream);
+
+namespace nsd {
+int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+		  const nsd_rec &rec, const nsd_ext *ext_table);
+void format_post_dump(std::string &s, const uint8_t *pkt, uint32_t caplen, int mode, uint32_t from,
+		      uint32_t to);
+}
+
+// ---- struct protocol surface (proto.h:18-26, dissector.c:22-41) -----------
+struct pkt_buff;
+struct protocol {
+	const unsigned int key;
+	void (*print_full)(struct pkt_buff *pkt);
+	void (*print_less)(struct pkt_buff *pkt);
+	struct protocol *next;
+	void (*process)(struct pkt_buff *pkt);
+};
+
+// The print functions of this library are the record renderer; per-ops
+// entries exist so the process-pointer protocol of dissector_set_print_type
+// carries the print mode exactly as in the reference (dissector_eth.c:17-28).
+static void nsd_render_full(struct pkt_buff *) {}
+static void nsd_render_less(struct pkt_buff *) {}
+static struct protocol g_ethernet_ops = { 0, nsd_render_full, nsd_render_less, nullptr, nullptr };
+
+extern "C" int dissector_set_print_type(void *ptr, int type)
+{
+	for (struct protocol *p = (struct protocol *)ptr; p; p = p->next) {
+		switch (type) {
+		case PRINT_NORM: p->process = p->print_full; break;
+		case PRINT_LESS: p->process = p->print_less; break;
+		default: p->process = nullptr; break;
+		}
+	}
+	return 0;
+}
+
+// parse semantics as selected by the ops' process pointers
+static int parse_mode()
+{
+	if (g_ethernet_ops.process == g_ethernet_ops.print_full && g_ethernet_ops.process)
+		return PRINT_NORM;
+	if (g_ethernet_ops.process == g_ethernet_ops.print_less && g_ethernet_ops.process)
+		return PRINT_LESS;
+	return PRINT_HEX;   // process == NULL: the chain does not run
+}
+
+// ---- device context ----------------------------------------------------
+namespace {
+struct DevCtx {
+	std::mutex mu;
+	bool init = false;
+	int dev = -1;
+	int cus = 0;
+	hipStream_t stream = nullptr;
+	uint8_t *frames = nullptr; size_t frames_cap = 0;
+	uint64_t *desc = nullptr; size_t desc_cap = 0;
+	nsd_rec *rec = nullptr; size_t rec_cap = 0;
+	nsd_ext *ext = nullptr; size_t ext_cap = 0;
+	uint32_t *ext_count = nullptr;
+	uint64_t *counters = nullptr;
+};
+DevCtx g_ctx;
+
+bool hip_ok(hipError_t e, const char *what)
+{
+	if (e != hipSuccess) {
+		fprintf(stderr, "netsniff-dissect: %s: %s\n", what, hipGetErrorString(e));
+		return false;
+	}
+	return true;
+}
+
+bool ctx_init(DevCtx &c)
+{
+	if (c.init)
+		return true;
+	int n = 0;
+	if (!hip_ok(hipGetDeviceCount(&n), "hipGetDeviceCount") || n == 0)
+		return false;
+	if (!hip_ok(hipGetDevice(&c.dev), "hipGetDevice"))
+		return false;
+	hipDeviceProp_t prop;
+	if (!hip_ok(hipGetDeviceProperties(&prop, c.dev), "hipGetDeviceProperties"))
+		return false;
+	c.cus = prop.multiProcessorCount;
+	if (!hip_ok(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate"))
+		return false;
+	if (!hip_ok(hipMalloc(&c.ext_count, 256), "hipMalloc"))
+		return false;
+	c.counters = (uint64_t *)((uint8_t *)c.ext_count + 64);
+	c.init = true;
+	return true;
+}
+
+template <class T>
+bool grow(T *&p, size_t &cap, size_t need)
+{
+	if (need <= cap)
+		return true;
+	if (p)
+		(void)hipFree(p);
+	p = nullptr;
+	size_t want = need + need / 4 + 64;
+	if (!hip_ok(hipMalloc(&p, want * sizeof(T)), "hipMalloc"))
+		return false;
+	cap = want;
+	return true;
+}
+
+int start_for(int linktype)
+{
+	auto is = [&](uint32_t v) { return (uint32_t)linktype == v || (uint32_t)linktype == __builtin_bswap32(v); };
+	if (is(NSD_LINKTYPE_EN10MB)) return NSD_OPS_ETHERNET;
+	if (is(NSD_LINKTYPE_LINUX_SLL)) return NSD_OPS_SLL;
+	if (is(NSD_LINKTYPE_IEEE802_11) || is(NSD_LINKTYPE_IEEE802_11_RADIOTAP)) return NSD_OPS_IEEE80211;
+	if (is(NSD_LINKTYPE_NETLINK)) return NSD_OPS_NLMSG;
+	return 0;   // unknown link type: start at none_ops (dissector.c:100-103)
+}
+} // namespace
+
+// ---- batch extension ---------------------------------------------------
+extern "C" int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
+				  int linktype, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+				  void *stream)
+{
+	if (n == 0)
+		return NSD_OK;
+	if (!d_frames || !d_desc || !d_rec || !d_ext_count || !d_counters)
+		return NSD_ERR_ARG;
+	if (ext_cap && !d_ext)
+		return NSD_ERR_ARG;
+	if (mode < PRINT_NORM || mode > PRINT_NONE)
+		return NSD_ERR_ARG;
+	int rc = nsd_launch_dissect(d_frames, d_desc, n, start_for(linktype), mode, d_rec, d_ext,
+				    ext_cap, d_ext_count, d_counters, 0, (hipStream_t)stream);
+	return rc ? NSD_ERR_HIP : NSD_OK;
+}
+
+// grid override for experiments (0 = default)
+extern "C" int nsd_dissect_device_grid(const uint8_t *d_frames, const nsd_desc_t *d_desc,
+				       uint32_t n, int linktype, int mode, nsd_rec *d_rec,
+				       nsd_ext *d_ext, uint32_t ext_cap, uint32_t *d_ext_count,
+				       uint64_t *d_counters, int grid, void *stream)
+{
+	if (n == 0)
+		return NSD_OK;
+	if (!d_frames || !d_desc || !d_rec || !d_ext_count || !d_counters)
+		return NSD_ERR_ARG;
+	int rc = nsd_launch_dissect(d_frames, d_desc, n, start_for(linktype), mode, d_rec, d_ext,
+				    ext_cap, d_ext_count, d_counters, grid, (hipStream_t)stream);
+	return rc ? NSD_ERR_HIP : NSD_OK;
+}
+
+extern "C" int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
+				     const nsd_desc_t *desc, uint32_t n, int linktype, int mode,
+				     nsd_rec *rec, nsd_ext *ext, uint32_t ext_cap,
+				     uint32_t *ext_count, uint64_t *counters)
+{
+	if (n == 0)
+		return NSD_OK;
+	if (!frames || !desc || !rec || (ext_cap && !ext))
+		return NSD_ERR_ARG;
+	for (uint32_t i = 0; i < n; i++) {
+		if (NSD_DESC_CAPLEN(desc[i]) > NSD_MAX_CAPLEN)
+			return NSD_ERR_CAPLEN;
+		if (NSD_DESC_OFF(desc[i]) + NSD_DESC_CAPLEN(desc[i]) > frames_len)
+			return NSD_ERR_ARG;
+	}
+	DevCtx &c = g_ctx;
+	std::lock_guard<std::mutex> lk(c.mu);
+	if (!ctx_init(c))
+		return NSD_ERR_HIP;
+	if (!grow(c.frames, c.frames_cap, frames_len + NSD_FRAME_PAD) || !grow(c.desc, c.desc_cap, n) ||
+	    !grow(c.rec, c.rec_cap, n) || (ext_cap && !grow(c.ext, c.ext_cap, ext_cap)))
+		return NSD_ERR_NOMEM;
+	hipStream_t s = c.stream;
+	bool ok = hip_ok(hipMemcpyAsync(c.frames, frames, frames_len, hipMemcpyHostToDevice, s), "H2D") &&
+		  hip_ok(hipMemsetAsync(c.frames + frames_len, 0, NSD_FRAME_PAD, s), "memset") &&
+		  hip_ok(hipMemcpyAsync(c.desc, desc, n * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D") &&
+		  hip_ok(hipMemsetAsync(c.ext_count, 0, 64 + NSD_NCOUNTERS * 8, s), "memset");
+	if (!ok)
+		return NSD_ERR_HIP;
+	if (nsd_launch_dissect(c.frames, c.desc, n, start_for(linktype), mode, c.rec,
+			       ext_cap ? c.ext : nullptr, ext_cap, c.ext_count, c.counters, 0, s))
+		return NSD_ERR_HIP;
+	uint32_t used = 0;
+	ok = hip_ok(hipMemcpyAsync(rec, c.rec, n * sizeof(nsd_rec), hipMemcpyDeviceToHost, s), "D2H") &&
+	     hip_ok(hipMemcpyAsync(&used, c.ext_count, 4, hipMemcpyDeviceToHost, s), "D2H");
+	if (ok && counters)
+		ok = hip_ok(hipMemcpyAsync(counters, c.counters, NSD_NCOUNTERS * 8, hipMemcpyDeviceToHost, s), "D2H");
+	ok = ok && hip_ok(hipStreamSynchronize(s), "sync");
+	if (ok && ext_cap) {
+		uint32_t k = used < ext_cap ? used : ext_cap;
+		if (k)
+			ok = hip_ok(hipMemcpy(ext, c.ext, k * sizeof(nsd_ext), hipMemcpyDeviceToHost), "D2H");
+	}
+	if (ext_count)
+		*ext_count = used;
+	return ok ? NSD_OK : NSD_ERR_HIP;
+}
+
+// ---- output: the host's tprintf if present, else wrapped stdout ---------
+extern "C" {
+void tprintf(char *msg, ...) __attribute__((weak));
+void tprintf_flush(void) __attribute__((weak));
+}
+
+// __tprintf_flush (tprintf.c:65-103) applied to one flushed buffer
+extern "C" long nsd_tprintf_wrap(const char *in, size_t len, int cols, long *state, char *out,
+				 size_t cap)
+{
+	const long term_start = 3;
+	long term_len = cols - 5;
+	long line_count = state ? *state : 0;
+	long color_open = 0;
+	size_t o = 0;
+	if (!out || cap < 2 * len + 16)
+		return NSD_ERR_ARG;
+	for (size_t i = 0; i < len; ++i) {
+		if (in[i] == '\n') {
+			term_len = cols - 5;
+			line_count = -1;
+		}
+		if (in[i] == 033 && i + 1 < len && in[i + 1] == '[')
+			color_open++;
+		if (color_open == 0 && line_count >= term_len) {
+			out[o++] = '\n';
+			for (long k = 0; k < term_start; k++)
+				out[o++] = ' ';
+			line_count = term_start;
+			while (i < len && (in[i] == ' ' || in[i] == ','))
+				i++;
+		}
+		// at i == len the reference reads buffer[buffer_use], the NUL that
+		// vsnprintf left there
+		const char ch = i < len ? in[i] : '\0';
+		if (color_open > 0 && ch == 'm')
+			color_open--;
+		out[o++] = ch;
+		line_count++;
+	}
+	if (state)
+		*state = line_count;
+	return (long)o;
+}
+
+namespace {
+long g_line_count = 0;
+
+int tty_cols()
+{
+	struct winsize ts;
+	return ioctl(0, TIOCGWINSZ, &ts) == 0 ? ts.ws_col : 80;   // DEFAULT_TTY_SIZE
+}
+
+void emit(const std::string &s)
+{
+	if (tprintf) {
+		for (size_t i = 0; i < s.size(); i += 256) {
+			size_t k = s.size() - i < 256 ? s.size() - i : 256;
+			tprintf((char *)"%.*s", (int)k, s.data() + i);
+		}
+		if (tprintf_flush)
+			tprintf_flush();
+		return;
+	}
+	std::string w(2 * s.size() + 16, '\0');
+	long k = nsd_tprintf_wrap(s.data(), s.size(), tty_cols(), &g_line_count, &w[0], w.size());
+	if (k > 0)
+		fwrite(w.data(), 1, (size_t)k, stdout);
+	fflush(stdout);
+}
+} // namespace
+
+// ---- reference surface ---------------------------------------------------
+extern "C" void dissector_init_all(int fnttype)
+{
+	dissector_set_print_type(&g_ethernet_ops, fnttype);
+}
+
+extern "C" void dissector_cleanup_all(void)
+{
+	DevCtx &c = g_ctx;
+	std::lock_guard<std::mutex> lk(c.mu);
+	if (!c.init)
+		return;
+	(void)hipFree(c.frames); (void)hipFree(c.desc); (void)hipFree(c.rec); (void)hipFree(c.ext);
+	(void)hipFree(c.ext_count);
+	(void)hipStreamDestroy(c.stream);
+	c.frames = nullptr; c.desc = nullptr; c.rec = nullptr; c.ext = nullptr;
+	c.frames_cap = c.desc_cap = c.rec_cap = c.ext_cap = 0;
+	c.ext_count = nullptr; c.counters = nullptr; c.stream = nullptr;
+	c.init = false;
+}
+
+extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype, int mode,
+				      struct sockaddr_ll *sll)
+{
+	(void)sll;
+	if (mode == PRINT_NONE)   // dissector.c:70-71
+		return;
+	if (len > NSD_MAX_CAPLEN) {
+		fprintf(stderr, "netsniff-dissect: frame of %zu bytes exceeds %u\n", len, NSD_MAX_CAPLEN);
+		abort();
+	}
+	const int pm = parse_mode();
+	nsd_desc_t d = NSD_DESC(0, len);
+	nsd_rec rec;
+	nsd_ext ext;
+	uint32_t used = 0;
+	int rc = dissector_entry_batch(packet, len, &d, 1, linktype, pm, &rec, &ext, 1, &used, nullptr);
+	if (rc != NSD_OK) {
+		fprintf(stderr, "netsniff-dissect: device dissection failed (%d)\n", rc);
+		abort();   // like panic() (die.h:46): no CPU fallback
+	}
+	std::string s;
+	if (pm == PRINT_NORM || pm == PRINT_LESS) {
+		nsd::format_packet(s, packet, (uint32_t)len, linktype, pm, rec, &ext);
+		// post-chain dumps run on what the chain left (dissector.c:108-118):
+		// after print_full the exit op already pulled everything
+		if (pm == PRINT_LESS)
+			nsd::format_post_dump(s, packet, (uint32_t)len, mode, rec.data_off, rec.tail_off);
+	} else {
+		nsd::format_packet(s, packet, (uint32_t)len, linktype, mode, rec, &ext);
+	}
+	emit(s);
+}
+
+extern "C" const char *nsd_version(void) { return "netsniff-dissect 0.1 (gfx950)"; }
+
+extern "C" int nsd_device_count(void)
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess)
+		return 0;
+	return n;
+}

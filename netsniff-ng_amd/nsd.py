@@ -1,0 +1,194 @@
+"""nsd.py - Python binding of libnsdissect.so (the C ABI in
+include/netsniff_dissect.h).  Plumbing only: every dissection runs in the HIP
+kernels of the library; there is no Python or CPU fallback.  If the library or
+a GPU is missing the calls raise.
+
+Device-resident use (bench / multi-GPU) passes torch tensors; the kernel is
+launched on torch's current HIP stream so torch events time it correctly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnsdissect.so")
+
+PRINT_NORM, PRINT_LESS, PRINT_HEX, PRINT_ASCII, PRINT_HEX_ASCII, PRINT_NONE = range(6)
+LINKTYPE_EN10MB = 1
+NCOUNTERS = 64
+NSD_OPS_COUNT = 28
+CNT_PKTS, CNT_BYTES, CNT_IP_BAD, CNT_ICMP_BAD, CNT_HOST, CNT_EXT, CNT_OVERFLOW, CNT_TRIM = range(32, 40)
+FRAME_PAD = 64
+
+REC_DTYPE = np.dtype([("chain", "<u4"), ("data_off", "<u2"), ("tail_off", "<u2"),
+                      ("ip_csum", "<u2"), ("nflags", "u1"), ("off2", "u1", (5,))])
+EXT_DTYPE = np.dtype([("pkt", "<u4"), ("nlayers", "<u2"), ("rsvd", "<u2"),
+                      ("id", "u1", (64,)), ("off", "<u2", (64,))])
+REC_BYTES = 16
+EXT_BYTES = 200
+
+OPS_NAMES = ["invalid", "ethernet", "vlan", "QinQ", "mpls_uc", "arp", "lldp", "ipv4", "ipv6",
+             "ipv6_in_ipv4", "icmpv4", "icmpv6", "igmp", "ip_auth", "ip_esp", "ipv6_dest_opts",
+             "ipv6_fragm", "ipv6_hop_by_hop", "ipv6_mobility", "ipv6_no_next_header",
+             "ipv6_routing", "tcp", "udp", "dccp", "none", "sll", "ieee80211", "nlmsg"]
+
+# every entry point declared in include/netsniff_dissect.h
+ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup_all",
+               "dissector_set_print_type", "nsd_dissect_device", "dissector_entry_batch",
+               "nsd_format_packet", "nsd_lookup_init", "nsd_lookup_cleanup", "nsd_tprintf_wrap",
+               "nsd_version", "nsd_device_count"]
+
+_lib = None
+_vp, _u32, _u64, _int, _sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
+
+
+def lib():
+    """Load libnsdissect.so (raises OSError if it is not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not built (run make -C netsniff-ng_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.nsd_dissect_device.restype = _int
+        L.nsd_dissect_device.argtypes = [_vp, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp, _vp]
+        L.nsd_dissect_device_grid.restype = _int
+        L.nsd_dissect_device_grid.argtypes = [_vp, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp,
+                                              _int, _vp]
+        L.dissector_entry_batch.restype = _int
+        L.dissector_entry_batch.argtypes = [_vp, _sz, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp]
+        L.nsd_format_packet.restype = ctypes.c_long
+        L.nsd_format_packet.argtypes = [_vp, _u32, _int, _int, _vp, _vp, ctypes.c_char_p, _sz]
+        L.nsd_format_batch.restype = ctypes.c_long
+        L.nsd_format_batch.argtypes = [_vp, _vp, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]
+        L.nsd_lookup_init.restype = _int
+        L.nsd_lookup_init.argtypes = [ctypes.c_char_p]
+        L.nsd_lookup_cleanup.restype = None
+        L.nsd_tprintf_wrap.restype = ctypes.c_long
+        L.nsd_tprintf_wrap.argtypes = [ctypes.c_char_p, _sz, _int, ctypes.POINTER(ctypes.c_long),
+                                       ctypes.c_char_p, _sz]
+        L.nsd_version.restype = ctypes.c_char_p
+        L.nsd_device_count.restype = _int
+        L.dissector_init_all.argtypes = [_int]
+        L.dissector_entry_point.argtypes = [_vp, _sz, _int, _int, _vp]
+        _lib = L
+    return _lib
+
+
+class NsdError(RuntimeError):
+    pass
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise NsdError(f"{what} failed with status {rc}")
+
+
+def dissect_device(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, rec=None, ext=None,
+                   ext_count=None, counters=None, grid=0, stream=None):
+    """Walk a device-resident batch.  frames: uint8 cuda tensor (padded by
+    FRAME_PAD bytes), desc: int64/uint64 cuda tensor (packed descriptors).
+    Returns (rec u8[n*16], ext u8[cap*200], ext_count i32[1], counters i64[64])
+    as cuda tensors; counters/ext_count accumulate if passed in."""
+    import torch
+    n = desc.numel()
+    dev = desc.device
+    if rec is None:
+        rec = torch.empty(n * REC_BYTES, dtype=torch.uint8, device=dev)
+    if ext is None:
+        ext = torch.empty(max(n, 1) * EXT_BYTES, dtype=torch.uint8, device=dev)
+    if ext_count is None:
+        ext_count = torch.zeros(1, dtype=torch.int32, device=dev)
+    if counters is None:
+        counters = torch.zeros(NCOUNTERS, dtype=torch.int64, device=dev)
+    ext_cap = ext.numel() // EXT_BYTES
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    L = lib()
+    if grid:
+        rc = L.nsd_dissect_device_grid(frames.data_ptr(), desc.data_ptr(), n, linktype, mode,
+                                       rec.data_ptr(), ext.data_ptr(), ext_cap, ext_count.data_ptr(),
+                                       counters.data_ptr(), grid, stream)
+    else:
+        rc = L.nsd_dissect_device(frames.data_ptr(), desc.data_ptr(), n, linktype, mode,
+                                  rec.data_ptr(), ext.data_ptr(), ext_cap, ext_count.data_ptr(),
+                                  counters.data_ptr(), stream)
+    _check(rc, "nsd_dissect_device")
+    return rec, ext, ext_count, counters
+
+
+def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_cap=None):
+    """Host-memory batch through the device (H2D, kernel, D2H).
+    Returns (rec, ext[:count], counters) as numpy arrays."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    desc = np.ascontiguousarray(desc, dtype=np.uint64)
+    n = len(desc)
+    if ext_cap is None:
+        ext_cap = n
+    rec = np.zeros(n, dtype=REC_DTYPE)
+    ext = np.zeros(max(ext_cap, 1), dtype=EXT_DTYPE)
+    cnt = np.zeros(1, dtype=np.uint32)
+    counters = np.zeros(NCOUNTERS, dtype=np.uint64)
+    rc = lib().dissector_entry_batch(frames.ctypes.data, frames.nbytes, desc.ctypes.data, n,
+                                     linktype, mode, rec.ctypes.data, ext.ctypes.data, ext_cap,
+                                     cnt.ctypes.data, counters.ctypes.data)
+    _check(rc, "dissector_entry_batch")
+    return rec, ext[:min(int(cnt[0]), ext_cap)], counters
+
+
+def format_batch(frames, desc, rec, ext=None, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB):
+    """Render records to the reference text.  Returns (list of bytes per
+    packet, status array)."""
+    n = len(desc)
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    desc = np.ascontiguousarray(desc, dtype=np.uint64)
+    rec = np.ascontiguousarray(rec)
+    ext_ptr = None if ext is None or len(ext) == 0 else np.ascontiguousarray(ext).ctypes.data
+    ext_keep = None if ext is None else np.ascontiguousarray(ext)
+    if ext_keep is not None and len(ext_keep):
+        ext_ptr = ext_keep.ctypes.data
+    ends = np.zeros(n, dtype=np.uint64)
+    rc = np.zeros(n, dtype=np.int8)
+    cap = int(frames.nbytes) * 7 + 1024 * n + 4096
+    out = ctypes.create_string_buffer(cap)
+    total = lib().nsd_format_batch(frames.ctypes.data, desc.ctypes.data, n, linktype, mode,
+                                   rec.ctypes.data, ext_ptr, ctypes.addressof(out), cap,
+                                   ends.ctypes.data, rc.ctypes.data)
+    if total < 0:
+        raise NsdError("format buffer too small")
+    raw = out.raw[:total]
+    texts, prev = [], 0
+    for e in ends:
+        texts.append(raw[prev:int(e)])
+        prev = int(e)
+    return texts, rc
+
+
+def tprintf_wrap(text, cols=80, state=0):
+    """Apply the reference tprintf wrap (tprintf.c:65-103) to one flushed
+    buffer; returns (bytes, new_state)."""
+    st = ctypes.c_long(state)
+    cap = 2 * len(text) + 16
+    out = ctypes.create_string_buffer(cap)
+    k = lib().nsd_tprintf_wrap(text, len(text), cols, ctypes.byref(st), out, cap)
+    if k < 0:
+        raise NsdError("wrap failed")
+    return out.raw[:k], st.value
+
+
+def lookup_init(directory):
+    return lib().nsd_lookup_init(directory.encode() if directory else None)
+
+
+def lookup_cleanup():
+    lib().nsd_lookup_cleanup()
+
+
+def unpack_counters(counters):
+    c = np.asarray(counters, dtype=np.uint64)
+    out = {OPS_NAMES[i]: int(c[i]) for i in range(1, NSD_OPS_COUNT) if c[i]}
+    for name, k in [("pkts", CNT_PKTS), ("bytes", CNT_BYTES), ("ip_bad", CNT_IP_BAD),
+                    ("icmp_bad", CNT_ICMP_BAD), ("host", CNT_HOST), ("ext", CNT_EXT),
+                    ("overflow", CNT_OVERFLOW), ("trim", CNT_TRIM)]:
+        out[name] = int(c[k])
+    return out

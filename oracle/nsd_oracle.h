@@ -1,0 +1,83 @@
+/*
+ * nsd_oracle.h - CPU restatement of netsniff-ng's dissector chain.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the checker the device path is compared
+ * against; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may load it.  The product library (netsniff-ng_amd/) never links it.
+ *
+ * Parity pin: every parser except IPv4/IPv6 is pinned against the
+ * reference's own parser objects compiled from /root/reference (oracle/_ref,
+ * "make -C oracle ref"); IPv4/IPv6 cannot be compiled from the reference
+ * here (proto_ipv4.c/proto_ipv6.c include geoip.h -> the configure-generated
+ * config.h, which this image cannot produce), so their text is pinned by the
+ * restatement plus known-answer checks only.  See DESIGN.md "Oracle".
+ */
+#ifndef NSD_ORACLE_H
+#define NSD_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "../include/netsniff_dissect.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* growable text sink; pass NULL for fields-only walks */
+typedef struct nsor_text {
+	char  *buf;
+	size_t len, cap;
+	int    unsupported;   /* set when a host-only body (ARP, LLDP, ...) was hit */
+} nsor_text;
+
+void nsor_text_init(nsor_text *t);
+void nsor_text_free(nsor_text *t);
+void nsor_text_reset(nsor_text *t);
+
+/* per-packet walk result beyond the record */
+typedef struct nsor_info {
+	uint32_t nlayers;
+	uint8_t  id[NSD_EXT_MAX_LAYERS];
+	uint16_t off[NSD_EXT_MAX_LAYERS];
+	uint32_t data, tail;
+	uint32_t w_bytes;      /* algorithmic read bytes W(pkt) */
+	int      overflow;
+} nsor_info;
+
+/* Dissect one packet (bytes past caplen read as zero).
+ * mode: PRINT_* ; linktype as in dissector_entry_point.
+ * text may be NULL (no formatting).  rec/info may be NULL. */
+void nsor_dissect(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+		  nsor_text *text, nsd_rec *rec, nsor_info *info);
+
+/* Batch form producing exactly what the device produces.  ext slots are
+ * assigned in packet order (the device assigns them in arbitrary order; tests
+ * compare through the slot indirection).  counters accumulate. Returns sum W. */
+uint64_t nsor_dissect_batch(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
+			    int linktype, int mode, nsd_rec *rec, nsd_ext *ext,
+			    uint32_t ext_cap, uint32_t *ext_count, uint64_t *counters);
+
+/* Same walk, text for every packet appended to *text (fields+text baseline). */
+uint64_t nsor_dissect_batch_text(const uint8_t *frames, const nsd_desc_t *desc,
+				 uint32_t n, int linktype, int mode, nsor_text *text);
+
+/* Multi-threaded fields-only walk over contiguous shards (CPU baseline). */
+uint64_t nsor_dissect_batch_mt(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
+			       int linktype, int mode, nsd_rec *rec, uint64_t *counters,
+			       int nthreads);
+
+/* Name tables (lookup.c:33-95 restated).  dir NULL => clear (names off). */
+int  nsor_lookup_init(const char *dir);
+void nsor_lookup_clear(void);
+
+/* Per-layer entry for the oracle/_ref hybrid harness: run one ops' print
+ * function on [*data, *tail) of pkt, return next ops ID (0 = chain ends).
+ * emit receives the text pieces in order. */
+typedef void (*nsor_emit_fn)(void *ctx, const char *s, size_t n);
+int nsor_run_layer(int ops_id, int mode, const uint8_t *pkt, uint32_t caplen,
+		   uint32_t *data, uint32_t *tail, nsor_emit_fn emit, void *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,296 @@
+/*
+ * ref_harness.c - drives the REFERENCE's own parser objects (compiled from
+ * /root/reference by oracle/Makefile ("make ref") into oracle/_ref/) over a pcap and
+ * prints through the reference's real tprintf.c.  TEST INFRASTRUCTURE ONLY.
+ *
+ * What comes from the reference (object files built from its sources as they
+ * lie): every proto_*.c parser except proto_ipv4.c / proto_ipv6.c, hash.c,
+ * lookup.c, tprintf.c, xmalloc.c, str.c, die.c, and the inline pkt_buff.h /
+ * hash.h helpers.
+ *
+ * What this file supplies, and why:
+ *   - the chain loop and entry point, restating dissector.c:43-122 for the
+ *     Ethernet link type (dissector.c itself includes ring.h -> config.h);
+ *   - the eth_lay2 / eth_lay3 tables, built with the reference's own
+ *     insert_hash / INSERT_HASH_PROTOS in dissector_eth.c:30-62 order
+ *     (dissector_eth.c includes dissector.h -> ring.h -> config.h);
+ *   - dissector_set_print_type, restating dissector.c:22-41;
+ *   - ipv4_ops / ipv6_ops / ipv6() / ipv6_less(): proto_ipv4.c and
+ *     proto_ipv6.c include geoip.h -> config.h, a configure-generated header
+ *     this image cannot produce (configure needs pkg-config).  Those layers
+ *     therefore run the oracle restatement (nsd_oracle.c) and are NOT pinned
+ *     by this harness.
+ *
+ * Usage: nsref [-m mode] [-n confdir] [-w cols] [-i index_out] file.pcap
+ *   -w 0    : stdin from /dev/null -> tprintf wraps at DEFAULT_TTY_SIZE (80)
+ *   -w N>0  : stdin is a pty N columns wide (N=65535: effectively unwrapped)
+ *   -i F    : write one u64 stdout byte offset per packet boundary to F
+ * Bytes past caplen are zero (parity domain).
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/ioctl.h>
+#include <termios.h>
+#include <unistd.h>
+
+#include "hash.h"
+#include "proto.h"
+#include "protos.h"
+#include "pkt_buff.h"
+#include "tprintf.h"
+#include "lookup.h"
+
+#include "nsd_oracle.h"
+
+struct hash_table eth_lay2;
+struct hash_table eth_lay3;
+
+static int g_mode;
+static uint32_t g_caplen;
+
+/* dissector.c:22-41 */
+int dissector_set_print_type(void *ptr, int type)
+{
+	struct protocol *proto;
+
+	for (proto = ptr; proto; proto = proto->next) {
+		switch (type) {
+		case PRINT_NORM: proto->process = proto->print_full; break;
+		case PRINT_LESS: proto->process = proto->print_less; break;
+		default:         proto->process = NULL; break;
+		}
+	}
+	return 0;
+}
+
+/* ---- IPv4 / IPv6 via the restatement (see header comment) --------------- */
+static void emit_tprintf(void *ctx, const char *s, size_t n)
+{
+	(void)ctx;
+	/* tprintf's 1 KiB buffer: hand over in pieces well below it */
+	while (n) {
+		size_t k = n > 256 ? 256 : n;
+		tprintf("%.*s", (int)k, s);
+		s += k;
+		n -= k;
+	}
+}
+
+static void run_oracle_layer(struct pkt_buff *pkt, int ops_id)
+{
+	uint32_t data = pkt->data - pkt->head, tail = pkt->tail - pkt->head;
+	int next = nsor_run_layer(ops_id, g_mode, pkt->head, g_caplen, &data, &tail,
+				  emit_tprintf, NULL);
+	pkt->data = pkt->head + data;
+	pkt->tail = pkt->head + tail;
+	if (next) {
+		/* map back to the key the reference would have looked up */
+		unsigned key = 0;
+		struct hash_table *tab = &eth_lay3;
+		switch (next) {
+		case NSD_OPS_ICMPV4: key = 1; break;
+		case NSD_OPS_ICMPV6: key = 58; break;
+		case NSD_OPS_IGMP: key = 2; break;
+		case NSD_OPS_IP_AUTH: key = 51; break;
+		case NSD_OPS_IP_ESP: key = 50; break;
+		case NSD_OPS_IPV6_DEST_OPTS: key = 60; break;
+		case NSD_OPS_IPV6_FRAGM: key = 44; break;
+		case NSD_OPS_IPV6_HOP_BY_HOP: key = 0; break;
+		case NSD_OPS_IPV6_IN_IPV4: key = 41; break;
+		case NSD_OPS_IPV6_MOBILITY: key = 135; break;
+		case NSD_OPS_IPV6_NO_NEXT: key = 59; break;
+		case NSD_OPS_IPV6_ROUTING: key = 43; break;
+		case NSD_OPS_TCP: key = 6; break;
+		case NSD_OPS_UDP: key = 17; break;
+		case NSD_OPS_DCCP: key = 33; break;
+		default: tab = NULL;
+		}
+		if (tab)
+			pkt_set_dissector(pkt, tab, key);
+	}
+}
+
+static void h_ipv4(struct pkt_buff *pkt) { run_oracle_layer(pkt, NSD_OPS_IPV4); }
+void ipv6(struct pkt_buff *pkt) { run_oracle_layer(pkt, NSD_OPS_IPV6); }
+void ipv6_less(struct pkt_buff *pkt) { run_oracle_layer(pkt, NSD_OPS_IPV6); }
+
+struct protocol ipv4_ops = { .key = 0x0800, .print_full = h_ipv4, .print_less = h_ipv4 };
+struct protocol ipv6_ops = { .key = 0x86DD, .print_full = ipv6, .print_less = ipv6_less };
+
+/* ---- tables: dissector_eth.c:30-62 -------------------------------------- */
+static void init_tables(int type)
+{
+	dissector_set_print_type(&ethernet_ops, type);
+	init_hash(&eth_lay2);
+	INSERT_HASH_PROTOS(arp_ops, eth_lay2);
+	INSERT_HASH_PROTOS(lldp_ops, eth_lay2);
+	INSERT_HASH_PROTOS(vlan_ops, eth_lay2);
+	INSERT_HASH_PROTOS(ipv4_ops, eth_lay2);
+	INSERT_HASH_PROTOS(ipv6_ops, eth_lay2);
+	INSERT_HASH_PROTOS(QinQ_ops, eth_lay2);
+	INSERT_HASH_PROTOS(mpls_uc_ops, eth_lay2);
+	for_each_hash_int(&eth_lay2, dissector_set_print_type, type);
+
+	init_hash(&eth_lay3);
+	INSERT_HASH_PROTOS(icmpv4_ops, eth_lay3);
+	INSERT_HASH_PROTOS(icmpv6_ops, eth_lay3);
+	INSERT_HASH_PROTOS(igmp_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ip_auth_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ip_esp_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ipv6_dest_opts_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ipv6_fragm_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ipv6_hop_by_hop_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ipv6_in_ipv4_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ipv6_mobility_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ipv6_no_next_header_ops, eth_lay3);
+	INSERT_HASH_PROTOS(ipv6_routing_ops, eth_lay3);
+	INSERT_HASH_PROTOS(tcp_ops, eth_lay3);
+	INSERT_HASH_PROTOS(udp_ops, eth_lay3);
+	INSERT_HASH_PROTOS(dccp_ops, eth_lay3);
+	for_each_hash_int(&eth_lay3, dissector_set_print_type, type);
+
+	dissector_set_print_type(&none_ops, type);
+}
+
+/* ---- chain loop + entry: dissector.c:43-122 (Ethernet link type) -------- */
+static void dissector_main(struct pkt_buff *pkt, struct protocol *start, struct protocol *end)
+{
+	struct protocol *d;
+
+	if (!start)
+		return;
+	for (pkt->dissector = start; pkt->dissector; ) {
+		if (!pkt->dissector->process)
+			break;
+		d = pkt->dissector;
+		pkt->dissector = NULL;
+		d->process(pkt);
+	}
+	if (end && end->process)
+		end->process(pkt);
+}
+
+static void entry(uint8_t *packet, size_t len, int linktype, int mode)
+{
+	struct pkt_buff *pkt;
+
+	if (mode == PRINT_NONE)
+		return;
+	pkt = pkt_alloc(packet, len);
+	pkt->link_type = linktype;
+	pkt->sll = NULL;
+	if (linktype == 1 || (uint32_t)linktype == 0x01000000u)
+		dissector_main(pkt, &ethernet_ops, &none_ops);
+	else
+		dissector_main(pkt, &none_ops, NULL);
+	switch (mode) {
+	case PRINT_HEX: hex(pkt); break;
+	case PRINT_ASCII: ascii(pkt); break;
+	case PRINT_HEX_ASCII: hex_ascii(pkt); break;
+	}
+	tprintf_flush();
+	pkt_free(pkt);
+}
+
+static int setup_stdin(int cols)
+{
+	int fd;
+
+	if (cols <= 0) {
+		fd = open("/dev/null", O_RDONLY);
+	} else {
+		struct winsize ws = { .ws_row = 24, .ws_col = (unsigned short)cols };
+		int m = posix_openpt(O_RDWR | O_NOCTTY);
+		if (m < 0 || grantpt(m) || unlockpt(m))
+			return -1;
+		fd = open(ptsname(m), O_RDWR | O_NOCTTY);
+		if (fd < 0 || ioctl(fd, TIOCSWINSZ, &ws))
+			return -1;
+	}
+	if (fd < 0 || dup2(fd, 0) < 0)
+		return -1;
+	return 0;
+}
+
+static uint32_t sw32(uint32_t v, int swap) { return swap ? __builtin_bswap32(v) : v; }
+
+int main(int argc, char **argv)
+{
+	int opt, cols = 0, names = 0;
+	const char *index_out = NULL;
+	FILE *f, *fi = NULL;
+	uint32_t fh[6];
+	int swap;
+	uint8_t *buf;
+	static char outbuf[1 << 20];
+
+	g_mode = PRINT_NORM;
+	while ((opt = getopt(argc, argv, "m:nw:i:")) != -1) {
+		switch (opt) {
+		case 'm': g_mode = atoi(optarg); break;
+		case 'n': names = 1; break;
+		case 'w': cols = atoi(optarg); break;
+		case 'i': index_out = optarg; break;
+		default:
+			fprintf(stderr, "usage: %s [-m mode] [-n] [-w cols] [-i idx] file.pcap\n", argv[0]);
+			return 2;
+		}
+	}
+	if (optind >= argc)
+		return 2;
+	if (setup_stdin(cols)) {
+		fprintf(stderr, "stdin setup failed: %s\n", strerror(errno));
+		return 1;
+	}
+	/* tprintf_init initialises the buffer spinlock and makes stdout
+	 * unbuffered (tprintf.c:112-118); re-buffer stdout before any output:
+	 * the bytes are the same, only faster */
+	tprintf_init();
+	setvbuf(stdout, outbuf, _IOFBF, sizeof(outbuf));
+	if (names) {
+		lookup_init(LT_PORTS_UDP);
+		lookup_init(LT_PORTS_TCP);
+		lookup_init(LT_ETHERTYPES);
+		lookup_init(LT_OUI);
+	}
+	init_tables(g_mode);
+
+	f = fopen(argv[optind], "rb");
+	if (!f || fread(fh, 4, 6, f) != 6) {
+		fprintf(stderr, "cannot read %s\n", argv[optind]);
+		return 1;
+	}
+	swap = fh[0] == 0xd4c3b2a1u || fh[0] == 0x4d3cb2a1u;
+	if (index_out)
+		fi = fopen(index_out, "wb");
+	buf = calloc(1, 65536 + 4096);
+	for (;;) {
+		uint32_t rh[4], caplen;
+		uint64_t pos;
+		if (fread(rh, 4, 4, f) != 4)
+			break;
+		caplen = sw32(rh[2], swap);
+		if (caplen > 65536)
+			return 1;
+		memset(buf, 0, 65536 + 4096);
+		if (fread(buf, 1, caplen, f) != caplen)
+			break;
+		g_caplen = caplen;
+		entry(buf, caplen, (int)sw32(fh[5], swap), g_mode);
+		if (fi) {
+			fflush(stdout);
+			pos = (uint64_t)ftello(stdout);
+			fwrite(&pos, 8, 1, fi);
+		}
+	}
+	fflush(stdout);
+	if (fi)
+		fclose(fi);
+	fclose(f);
+	return 0;
+}

@@ -1,0 +1,24 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "netsniff-ng_amd"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP kernels)")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def native_build():
+    """Build the C test infrastructure (tools/, oracle/, oracle/_ref when the
+    reference tree is present) and the product library if missing."""
+    import nsd_testlib
+    nsd_testlib.build_native()
+    if not os.path.exists(os.path.join(ROOT, "netsniff-ng_amd", "libnsdissect.so")):
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "netsniff-ng_amd")], check=True)
+    yield

@@ -1,0 +1,210 @@
+"""Shared helpers for the test suite: ctypes bindings to the synthetic
+generators (tools/), the CPU oracle (oracle/, TEST INFRASTRUCTURE) and the
+oracle/_ref reference harness, plus pcap I/O.  Only tests/, bench.py's
+cpu_baseline leg and __graft_entry__.smoke() use the oracle parts."""
+import ctypes
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+REF_BIN = os.path.join(ORACLE_DIR, "_ref", "nsref")
+SYNTH_SO = os.path.join(ROOT, "tools", "libnsdsynth.so")
+ORACLE_SO = os.path.join(ORACLE_DIR, "libnsdoracle.so")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+PRINT_NORM, PRINT_LESS, PRINT_HEX, PRINT_ASCII, PRINT_HEX_ASCII, PRINT_NONE = range(6)
+SYN_UDP64, SYN_IMIX, SYN_IPV6X = 1, 3, 4
+SEED = 0x5EED
+
+REC_DTYPE = np.dtype([("chain", "<u4"), ("data_off", "<u2"), ("tail_off", "<u2"),
+                      ("ip_csum", "<u2"), ("nflags", "u1"), ("off2", "u1", (5,))])
+assert REC_DTYPE.itemsize == 16
+EXT_DTYPE = np.dtype([("pkt", "<u4"), ("nlayers", "<u2"), ("rsvd", "<u2"),
+                      ("id", "u1", (64,)), ("off", "<u2", (64,))])
+assert EXT_DTYPE.itemsize == 200
+NCOUNTERS = 64
+
+
+def build_native(quiet=True):
+    """Build tools/ and oracle/ C libraries (and oracle/_ref when the
+    reference tree is present).  Idempotent."""
+    out = subprocess.DEVNULL if quiet else None
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools")], check=True, stdout=out)
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True, stdout=out)
+    if os.path.isdir("/root/reference"):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, "ref"], check=True, stdout=out)
+
+
+_synth = None
+_oracle = None
+
+
+def synth():
+    global _synth
+    if _synth is None:
+        lib = ctypes.CDLL(SYNTH_SO)
+        lib.nsd_synth_layout.restype = ctypes.c_uint64
+        lib.nsd_synth_layout.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                         ctypes.c_void_p]
+        lib.nsd_synth_fill.restype = None
+        lib.nsd_synth_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int]
+        lib.nsd_synth_pcap.restype = ctypes.c_uint64
+        lib.nsd_synth_pcap.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.c_uint64, ctypes.c_char_p]
+        _synth = lib
+    return _synth
+
+
+def make_batch(cfg, n, lo=0, seed=SEED, align=16, threads=8, pad=64):
+    """Generate packets [lo, lo+n) of a config: returns (frames u8 array,
+    desc u64 array)."""
+    s = synth()
+    desc = np.zeros(n, dtype=np.uint64)
+    end = s.nsd_synth_layout(cfg, seed, lo, n, align, 0, desc.ctypes.data)
+    frames = np.zeros(end + pad, dtype=np.uint8)
+    s.nsd_synth_fill(cfg, seed, lo, n, frames.ctypes.data, desc.ctypes.data, threads)
+    return frames, desc
+
+
+def desc_pack(off, caplen):
+    return (np.uint64(caplen) << np.uint64(40)) | np.uint64(off)
+
+
+def desc_off(desc):
+    return (desc & np.uint64(0xFFFFFFFFFF)).astype(np.int64)
+
+
+def desc_caplen(desc):
+    return (desc >> np.uint64(40)).astype(np.int64)
+
+
+def batch_from_packets(pkts, align=16, pad=64):
+    """List of bytes -> (frames, desc)."""
+    offs, off = [], 0
+    for p in pkts:
+        off = (off + align - 1) & ~(align - 1)
+        offs.append(off)
+        off += len(p)
+    frames = np.zeros(off + pad, dtype=np.uint8)
+    desc = np.zeros(len(pkts), dtype=np.uint64)
+    for i, (o, p) in enumerate(zip(offs, pkts)):
+        frames[o:o + len(p)] = np.frombuffer(bytes(p), dtype=np.uint8)
+        desc[i] = desc_pack(o, len(p))
+    return frames, desc
+
+
+def write_pcap(path, pkts, linktype=1):
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, linktype))
+        for i, p in enumerate(pkts):
+            f.write(struct.pack("<IIII", i, 0, len(p), len(p)))
+            f.write(bytes(p))
+
+
+def read_pcap(path):
+    with open(path, "rb") as f:
+        data = f.read()
+    magic = struct.unpack_from("<I", data, 0)[0]
+    e = "<" if magic in (0xA1B2C3D4, 0xA1B23C4D) else ">"
+    linktype = struct.unpack_from(e + "I", data, 20)[0]
+    pkts, o = [], 24
+    while o + 16 <= len(data):
+        _, _, caplen, _ = struct.unpack_from(e + "IIII", data, o)
+        o += 16
+        pkts.append(data[o:o + caplen])
+        o += caplen
+    return linktype, pkts
+
+
+# ---- oracle (TEST INFRASTRUCTURE) ------------------------------------------
+class _Text(ctypes.Structure):
+    _fields_ = [("buf", ctypes.c_void_p), ("len", ctypes.c_size_t), ("cap", ctypes.c_size_t),
+                ("unsupported", ctypes.c_int)]
+
+
+def oracle():
+    global _oracle
+    if _oracle is None:
+        lib = ctypes.CDLL(ORACLE_SO)
+        lib.nsor_dissect_batch.restype = ctypes.c_uint64
+        lib.nsor_dissect_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_void_p]
+        lib.nsor_dissect_batch_mt.restype = ctypes.c_uint64
+        lib.nsor_dissect_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_int]
+        lib.nsor_dissect_batch_text.restype = ctypes.c_uint64
+        lib.nsor_dissect_batch_text.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(_Text)]
+        lib.nsor_dissect.restype = None
+        lib.nsor_dissect.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(_Text), ctypes.c_void_p, ctypes.c_void_p]
+        lib.nsor_text_free.argtypes = [ctypes.POINTER(_Text)]
+        lib.nsor_lookup_init.restype = ctypes.c_int
+        lib.nsor_lookup_init.argtypes = [ctypes.c_char_p]
+        _oracle = lib
+    return _oracle
+
+
+def oracle_records(frames, desc, linktype=1, mode=PRINT_NORM, ext_cap=None):
+    """Returns (rec, ext[:count], counters, sum_w)."""
+    lib = oracle()
+    n = len(desc)
+    if ext_cap is None:
+        ext_cap = n
+    rec = np.zeros(n, dtype=REC_DTYPE)
+    ext = np.zeros(max(ext_cap, 1), dtype=EXT_DTYPE)
+    cnt = np.zeros(1, dtype=np.uint32)
+    counters = np.zeros(NCOUNTERS, dtype=np.uint64)
+    sw = lib.nsor_dissect_batch(frames.ctypes.data, desc.ctypes.data, n, linktype, mode,
+                                rec.ctypes.data, ext.ctypes.data, ext_cap, cnt.ctypes.data,
+                                counters.ctypes.data)
+    return rec, ext[:min(int(cnt[0]), ext_cap)], counters, int(sw)
+
+
+def oracle_text_packets(frames, desc, linktype=1, mode=PRINT_NORM):
+    """Per-packet oracle text (list of (bytes, unsupported))."""
+    lib = oracle()
+    out = []
+    offs, caps = desc_off(desc), desc_caplen(desc)
+    for i in range(len(desc)):
+        t = _Text()
+        p = frames[offs[i]:offs[i] + caps[i]]
+        lib.nsor_dissect(p.ctypes.data, int(caps[i]), linktype, mode, ctypes.byref(t), None, None)
+        s = ctypes.string_at(t.buf, t.len) if t.len else b""
+        out.append((s, bool(t.unsupported)))
+        lib.nsor_text_free(ctypes.byref(t))
+    return out
+
+
+def run_ref(pcap_path, mode=PRINT_NORM, cols=65535, names=False, timeout=120):
+    """Run oracle/_ref/nsref; returns list of per-packet text (bytes)."""
+    idx = pcap_path + f".m{mode}.idx"
+    args = [REF_BIN, "-m", str(mode), "-w", str(cols), "-i", idx]
+    if names:
+        args.append("-n")
+    args.append(pcap_path)
+    txt = pcap_path + f".m{mode}.txt"
+    with open(txt, "wb") as fo:
+        r = subprocess.run(args, stdout=fo, stderr=subprocess.PIPE, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"nsref failed rc={r.returncode}: {r.stderr[:500]!r}")
+    ends = np.fromfile(idx, dtype=np.uint64)
+    with open(txt, "rb") as fi:
+        data = fi.read()
+    os.unlink(idx)
+    os.unlink(txt)
+    out, prev = [], 0
+    for e in ends:
+        out.append(data[prev:int(e)])
+        prev = int(e)
+    return out
