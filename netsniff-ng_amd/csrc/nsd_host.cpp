@@ -111,7 +111,7 @@ bool ctx_init(DevCtx &c)
 	c.cus = prop.multiProcessorCount;
 	if (!hip_ok(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking), "hipStreamCreate"))
 		return false;
-	if (!hip_ok(hipMalloc(&c.ext_count, 256), "hipMalloc"))
+	if (!hip_ok(hipMalloc(&c.ext_count, 1024), "hipMalloc"))
 		return false;
 	c.counters = (uint64_t *)((uint8_t *)c.ext_count + 64);
 	c.init = true;

@@ -125,9 +125,7 @@ __device__ __forceinline__ void record_layer(WalkOut &w, int id, const ExtSink &
 template <class Src>
 __device__ __forceinline__ uint16_t calc_csum(const Src &s, uint32_t off, uint32_t nwords)
 {
-	uint32_t sum = 0;   // <= 32767 words * 0xffff fits in 32 bits
-	for (uint32_t i = 0; i < nwords; i++)
-		sum += s.le16(off + 2 * i);
+	uint32_t sum = s.sum16(off, nwords);   // <= 32767 words * 0xffff fits in 32 bits
 	sum = (sum >> 16) + (sum & 0xffff);
 	sum += (sum >> 16);
 	return (uint16_t)~sum;
@@ -154,14 +152,12 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 	int id = start_id;
 	while (id) {
 		record_layer(w, id, es);
-		const bool counted = w.n <= NSD_EXT_MAX_LAYERS;   // oracle counts the first 64
-#define NSD_COUNT(ID) do { if (counted) cnt.template inc<ID>(); } while (0)
+		cnt(w.n <= NSD_EXT_MAX_LAYERS ? id : -1);   // the oracle counts the first 64 layers
 		const uint32_t start = w.data;
 		const uint32_t len = w.tail - w.data;   // pkt_len (pkt_buff.h:36-41)
 		int next = 0;
 		switch (id) {
 		case NSD_OPS_ETHERNET:      // proto_ethernet.c:48-79
-			NSD_COUNT(NSD_OPS_ETHERNET);
 			if (len >= 14) {
 				next = lay2(s.be16(start + 12));
 				w.data = start + 14;
@@ -169,14 +165,12 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			break;
 		case NSD_OPS_VLAN:          // proto_vlan.c:22-40
 		case NSD_OPS_QINQ:          // proto_vlan_q_in_q.c:23-41
-			if (id == NSD_OPS_VLAN) NSD_COUNT(NSD_OPS_VLAN); else NSD_COUNT(NSD_OPS_QINQ);
 			if (len >= 4) {
 				next = lay2(s.be16(start + 2));
 				w.data = start + 4;
 			}
 			break;
 		case NSD_OPS_MPLS_UC: {     // proto_mpls_unicast.c:49-77
-			NSD_COUNT(NSD_OPS_MPLS_UC);
 			uint32_t d = start, l = len;
 			bool ok = true;
 			for (;;) {
@@ -193,7 +187,6 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			break;
 		}
 		case NSD_OPS_IPV4: {        // proto_ipv4.c:34-178 / 180-204
-			NSD_COUNT(NSD_OPS_IPV4);
 			if (len < 20)
 				break;
 			const uint8_t ihl = s.b(start) & 0xF;
@@ -217,7 +210,6 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 		}
 		case NSD_OPS_IPV6:          // proto_ipv6.c:22-105
 		case NSD_OPS_IPV6_IN_IPV4:  // proto_ipv6_in_ipv4.c:20-24
-			if (id == NSD_OPS_IPV6) NSD_COUNT(NSD_OPS_IPV6); else NSD_COUNT(NSD_OPS_IPV6_IN_IPV4);
 			if (len >= 40) {
 				next = lay3(s.b(start + 6));
 				w.data = start + 40;
@@ -225,8 +217,6 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			break;
 		case NSD_OPS_IPV6_HOP_BY_HOP:   // proto_ipv6_hop_by_hop.c:39-71
 		case NSD_OPS_IPV6_DEST_OPTS: {  // proto_ipv6_dest_opts.c:40-72
-			if (id == NSD_OPS_IPV6_HOP_BY_HOP) NSD_COUNT(NSD_OPS_IPV6_HOP_BY_HOP);
-			else NSD_COUNT(NSD_OPS_IPV6_DEST_OPTS);
 			if (len < 2)
 				break;
 			const uint32_t opt_len = (s.b(start + 1) + 1u) * 8u - 2u;
@@ -238,7 +228,6 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			break;
 		}
 		case NSD_OPS_IPV6_ROUTING: {    // proto_ipv6_routing.c:79-122
-			NSD_COUNT(NSD_OPS_IPV6_ROUTING);
 			if (len < 4)
 				break;
 			const uint32_t data_len = (s.b(start + 1) + 1u) * 8u - 4u;
@@ -251,14 +240,12 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			break;
 		}
 		case NSD_OPS_IPV6_FRAGM:    // proto_ipv6_fragm.c:25-47
-			NSD_COUNT(NSD_OPS_IPV6_FRAGM);
 			if (len >= 8) {
 				next = lay3(s.b(start));
 				w.data = start + 8;
 			}
 			break;
 		case NSD_OPS_IP_AUTH: {     // proto_ip_authentication_hdr.c:26-69
-			NSD_COUNT(NSD_OPS_IP_AUTH);
 			if (len < 12)
 				break;
 			const uint32_t hdr_len = s.b(start + 1) * 4u + 8u;
@@ -271,15 +258,12 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			break;
 		}
 		case NSD_OPS_IP_ESP:        // proto_ip_esp.c:23-35: leaf
-			NSD_COUNT(NSD_OPS_IP_ESP);
 			if (len >= 8)
 				w.data = start + 8;
 			break;
 		case NSD_OPS_IPV6_NO_NEXT:  // proto_ipv6_no_nxt_hdr.c:17-29: leaf, no pull
-			NSD_COUNT(NSD_OPS_IPV6_NO_NEXT);
 			break;
 		case NSD_OPS_IPV6_MOBILITY: {   // proto_ipv6_mobility_hdr.c:247-309
-			NSD_COUNT(NSD_OPS_IPV6_MOBILITY);
 			if (len < 6)
 				break;
 			const int32_t hdr_ext_len = (s.b(start + 1) + 1) * 8;
@@ -314,17 +298,14 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			break;
 		}
 		case NSD_OPS_TCP:           // proto_tcp.c:63-107: leaf, options not pulled
-			NSD_COUNT(NSD_OPS_TCP);
 			if (len >= 20)
 				w.data = start + 20;
 			break;
 		case NSD_OPS_UDP:           // proto_udp.c:23-58: leaf
-			NSD_COUNT(NSD_OPS_UDP);
 			if (len >= 8)
 				w.data = start + 8;
 			break;
 		case NSD_OPS_ICMPV4:        // proto_icmpv4.c:34-51: leaf
-			NSD_COUNT(NSD_OPS_ICMPV4);
 			if (len >= 8) {
 				w.data = start + 8;
 				if (MODE == PRINT_NORM) {
@@ -336,7 +317,6 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			}
 			break;
 		case NSD_OPS_ICMPV6: {      // proto_icmpv6.c:1667-1699: leaf
-			NSD_COUNT(NSD_OPS_ICMPV6);
 			if (len < 4)
 				break;
 			w.data = start + 4;
@@ -355,13 +335,11 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 		}
 		default:
 			// ARP, LLDP, IGMP, DCCP and non-Ethernet heads: host-rendered leaves
-			if (counted) cnt.any(id);
 			w.flags |= NSD_F_HOST;
 			w.data = start;
 			break;
 		}
 		id = next;
-#undef NSD_COUNT
 	}
 }
 

@@ -1,0 +1,110 @@
+"""Regenerate the committed golden fixtures (run in the build container, where
+/root/reference exists and oracle/_ref/nsref is built):
+
+  tiny.pcap            C1: 1000 x 64 B Eth/IPv4/UDP
+  edge.pcap            tests/edge_cases.py (every §8a quirk)
+  <pcap>.m<M>.w<C>.txt.gz / .ends.json
+                       text printed by the REFERENCE parser objects
+                       (oracle/_ref/nsref) for print mode M, terminal width C
+                       (65535 = unwrapped, 80 = tprintf's default wrap),
+                       names off (no conf files);  .names. = conf files of
+                       /root/reference loaded
+  prefix.json          SHA-256 of the nsref text of the first 65536 packets of
+                       C2/C3/C4 (NORM, LESS) and of the oracle records / counters
+  wsum.json            sum of W(pkt) (algorithmic read bytes) over
+                       the 16M-packet shards used by bench.py
+
+IPv4/IPv6 layers inside nsref come from the restatement (their reference
+sources need the configure-generated config.h); see oracle/ref_harness.c.
+"""
+import gzip
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import edge_cases  # noqa: E402
+import nsd_testlib as T  # noqa: E402
+
+MODES = [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX, T.PRINT_ASCII, T.PRINT_HEX_ASCII]
+
+
+def save_text(base, texts):
+    ends, off = [], 0
+    for t in texts:
+        off += len(t)
+        ends.append(off)
+    with gzip.open(base + ".txt.gz", "wb", compresslevel=9) as f:
+        f.write(b"".join(texts))
+    with open(base + ".ends.json", "w") as f:
+        json.dump(ends, f)
+
+
+def rec_digest(rec, ext):
+    """Records with ext slots replaced by the slot's content (slot order is
+    arbitrary on the device)."""
+    h = hashlib.sha256()
+    for i in range(len(rec)):
+        r = rec[i]
+        if (int(r["nflags"]) & 7) == 7:
+            slot = int.from_bytes(bytes(r["off2"][:4]), "little")
+            h.update(r.tobytes()[:11])
+            if slot != 0xFFFFFFFF:
+                e = ext[slot]
+                m = int(e["nlayers"])
+                h.update(e["id"][:m].tobytes() + e["off"][:m].tobytes())
+        else:
+            h.update(r.tobytes())
+    return h.hexdigest()
+
+
+def main():
+    T.build_native()
+    tiny = os.path.join(HERE, "tiny.pcap")
+    edge = os.path.join(HERE, "edge.pcap")
+    T.synth().nsd_synth_pcap(T.SYN_UDP64, T.SEED, 0, 1000, tiny.encode())
+    T.write_pcap(edge, edge_cases.cases())
+    for pcap in (tiny, edge):
+        stem = os.path.splitext(pcap)[0]
+        for m in MODES:
+            save_text(f"{stem}.m{m}.w65535", T.run_ref(pcap, mode=m, cols=65535))
+        for m in (T.PRINT_NORM, T.PRINT_LESS):
+            save_text(f"{stem}.m{m}.w80", T.run_ref(pcap, mode=m, cols=0))
+            save_text(f"{stem}.names.m{m}.w65535", T.run_ref(pcap, mode=m, cols=65535, names=True))
+
+    prefix = {}
+    for key, cfg in (("udp64", T.SYN_UDP64), ("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):
+        path = f"/tmp/golden_{key}.pcap"
+        T.synth().nsd_synth_pcap(cfg, T.SEED, 0, 65536, path.encode())
+        frames, desc = T.make_batch(cfg, 65536)
+        for m in (T.PRINT_NORM, T.PRINT_LESS):
+            txt = b"".join(T.run_ref(path, mode=m, cols=65535, timeout=600))
+            rec, ext, cnt, sw = T.oracle_records(frames, desc, mode=m)
+            prefix[f"{key}:m{m}"] = {"text_sha256": hashlib.sha256(txt).hexdigest(),
+                                     "records_sha256": rec_digest(rec, ext),
+                                     "counters": [int(x) for x in cnt], "wsum": sw}
+        os.unlink(path)
+    with open(os.path.join(HERE, "prefix.json"), "w") as f:
+        json.dump(prefix, f, indent=1)
+
+    wsum = {}
+    n = 1 << 24
+    for key, cfg, shards in (("imix", T.SYN_IMIX, 8), ("ipv6x", T.SYN_IPV6X, 1)):
+        for r in range(shards):
+            frames, desc = T.make_batch(cfg, n, lo=r * n)
+            counters = np.zeros(64, dtype=np.uint64)
+            sw = T.oracle().nsor_dissect_batch_mt(frames.ctypes.data, desc.ctypes.data, n, 1,
+                                                  T.PRINT_NORM, None, counters.ctypes.data, 8)
+            wsum[f"{key}:{r * n}:{n}"] = int(sw)
+            del frames, desc
+            print(key, r, sw, flush=True)
+    with open(os.path.join(HERE, "wsum.json"), "w") as f:
+        json.dump(wsum, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+"""CPU tests against the committed golden fixtures (tests/golden/, produced by
+the reference's own parser objects via oracle/_ref/nsref, make_golden.py):
+
+  - the oracle restatement reproduces the golden text (pins the oracle);
+  - the PRODUCT host formatter, fed the oracle's records, reproduces it too;
+  - the product tprintf wrap emulation reproduces the 80-column text;
+  - names-on flavour (conf files) where /root/reference exists.
+"""
+import gzip
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import nsd
+import nsd_testlib as T
+
+G = T.GOLDEN
+MODES = [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX, T.PRINT_ASCII, T.PRINT_HEX_ASCII]
+REF_CONF = "/root/reference"
+
+
+def load_golden(base):
+    with gzip.open(os.path.join(G, base + ".txt.gz"), "rb") as f:
+        data = f.read()
+    with open(os.path.join(G, base + ".ends.json")) as f:
+        ends = json.load(f)
+    out, prev = [], 0
+    for e in ends:
+        out.append(data[prev:e])
+        prev = e
+    return out
+
+
+def batch(name):
+    lt, pkts = T.read_pcap(os.path.join(G, name + ".pcap"))
+    frames, desc = T.batch_from_packets(pkts)
+    return lt, pkts, frames, desc
+
+
+def host_only(texts_unsupported):
+    return {i for i, (_, u) in enumerate(texts_unsupported) if u}
+
+
+@pytest.mark.parametrize("name", ["tiny", "edge"])
+@pytest.mark.parametrize("mode", MODES)
+def test_oracle_matches_golden(name, mode):
+    lt, pkts, frames, desc = batch(name)
+    gold = load_golden(f"{name}.m{mode}.w65535")
+    ora = T.oracle_text_packets(frames, desc, linktype=lt, mode=mode)
+    assert len(gold) == len(pkts)
+    bad = [i for i, (t, unsup) in enumerate(ora) if not unsup and t != gold[i]]
+    assert not bad, f"oracle text differs at {bad[:10]}"
+    if name == "tiny":
+        assert not host_only(ora)
+
+
+@pytest.mark.parametrize("name", ["tiny", "edge"])
+@pytest.mark.parametrize("mode", MODES)
+def test_formatter_matches_golden(name, mode):
+    """Product formatter (record + raw bytes -> text) vs reference text."""
+    lt, pkts, frames, desc = batch(name)
+    gold = load_golden(f"{name}.m{mode}.w65535")
+    rec, ext, _, _ = T.oracle_records(frames, desc, linktype=lt, mode=mode)
+    texts, rc = nsd.format_batch(frames, desc, rec, ext, mode=mode, linktype=lt)
+    ora = T.oracle_text_packets(frames, desc, linktype=lt, mode=mode)
+    skip = host_only(ora) | {i for i in range(len(rec)) if rec[i]["nflags"] & 0x20}
+    for i in range(len(pkts)):
+        if i in skip:
+            assert rc[i] != 0
+            continue
+        assert rc[i] == 0, f"packet {i}: formatter status {rc[i]}"
+        assert texts[i] == gold[i], f"packet {i} differs"
+    if name == "tiny":
+        assert not skip
+
+
+@pytest.mark.parametrize("name", ["tiny", "edge"])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_wrap_matches_golden(name, mode):
+    """tprintf's 80-column wrapping (tprintf.c:65-103) over the unwrapped
+    stream, carrying the line counter across packets."""
+    unwrapped = load_golden(f"{name}.m{mode}.w65535")
+    wrapped = load_golden(f"{name}.m{mode}.w80")
+    lt, pkts, frames, desc = batch(name)
+    ora = T.oracle_text_packets(frames, desc, linktype=lt, mode=mode)
+    state = 0
+    for i, (u, w) in enumerate(zip(unwrapped, wrapped)):
+        got, state = nsd.tprintf_wrap(u, cols=80, state=state)
+        if ora[i][1]:
+            state = 0 if w.endswith(b"\n") else state
+            continue
+        assert got == w, f"packet {i}: wrap differs"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CONF), reason="conf files live in /root/reference")
+@pytest.mark.parametrize("name", ["tiny", "edge"])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_names_on(name, mode):
+    lt, pkts, frames, desc = batch(name)
+    gold = load_golden(f"{name}.names.m{mode}.w65535")
+    try:
+        assert nsd.lookup_init(REF_CONF) == 4
+        assert T.oracle().nsor_lookup_init(REF_CONF.encode()) == 4
+        rec, ext, _, _ = T.oracle_records(frames, desc, linktype=lt, mode=mode)
+        texts, rc = nsd.format_batch(frames, desc, rec, ext, mode=mode, linktype=lt)
+        ora = T.oracle_text_packets(frames, desc, linktype=lt, mode=mode)
+    finally:
+        nsd.lookup_cleanup()
+        T.oracle().nsor_lookup_init(None)
+    for i in range(len(pkts)):
+        if ora[i][1] or rec[i]["nflags"] & 0x20:
+            continue
+        assert ora[i][0] == gold[i], f"oracle packet {i}"
+        assert rc[i] == 0 and texts[i] == gold[i], f"formatter packet {i}"
+
+
+def test_prefix_digests():
+    """64K-packet prefixes of C2/C3/C4: oracle records + counters + ΣW match
+    the committed digests (text digests were taken from nsref)."""
+    import make_golden_shim as mg
+    with open(os.path.join(G, "prefix.json")) as f:
+        want = json.load(f)
+    for key, cfg in (("udp64", T.SYN_UDP64), ("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):
+        frames, desc = T.make_batch(cfg, 65536)
+        for m in (T.PRINT_NORM, T.PRINT_LESS):
+            rec, ext, cnt, sw = T.oracle_records(frames, desc, mode=m)
+            w = want[f"{key}:m{m}"]
+            assert mg.rec_digest(rec, ext) == w["records_sha256"], key
+            assert [int(x) for x in cnt] == w["counters"], key
+            assert sw == w["wsum"], key
+
+
+@pytest.mark.parametrize("key,cfg", [("udp64", T.SYN_UDP64), ("imix", T.SYN_IMIX)])
+def test_prefix_text_formatter(key, cfg):
+    """Product formatter over 64K prefixes reproduces the nsref text digest."""
+    with open(os.path.join(G, "prefix.json")) as f:
+        want = json.load(f)
+    frames, desc = T.make_batch(cfg, 65536)
+    for m in (T.PRINT_NORM, T.PRINT_LESS):
+        rec, ext, _, _ = T.oracle_records(frames, desc, mode=m)
+        texts, rc = nsd.format_batch(frames, desc, rec, ext, mode=m)
+        assert (rc == 0).all()
+        assert hashlib.sha256(b"".join(texts)).hexdigest() == want[f"{key}:m{m}"]["text_sha256"]

@@ -17,4 +17,11 @@ if [ -n "$PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu ${BENCH_ARGS} > "$R/gpurun_out/prof.log" 2>&1; rc=$?
   echo "prof rc=$rc"; tail -n 5 "$R/gpurun_out/prof.log"; fatal $rc prof
 fi
+if [ -n "$PMC" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace -d "$R/gpurun_out/pmc_$ctr" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu ${BENCH_ARGS} > "$R/gpurun_out/pmc_$ctr.log" 2>&1; rc=$?
+    echo "pmc $ctr rc=$rc"; tail -n 3 "$R/gpurun_out/pmc_$ctr.log"; fatal $rc pmc
+  done
+fi
 exit 0
