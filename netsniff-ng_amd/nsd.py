@@ -47,6 +47,13 @@ def lib():
     """Load libnsdissect.so (raises OSError if it is not built)."""
     global _lib
     if _lib is None:
+        # torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's):
+        # whichever is loaded first serves the whole process, so let torch's
+        # runtime load first when torch is installed
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} not built (run make -C netsniff-ng_amd)")
         L = ctypes.CDLL(LIB_PATH)
