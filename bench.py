@@ -104,6 +104,7 @@ def main():
     ext = torch.empty(ext_cap * nsd.EXT_BYTES, dtype=torch.uint8, device=dev)
     ext_count = torch.zeros(1, dtype=torch.int32, device=dev)
     counters = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device=dev)
+    workspace = torch.empty(nsd.lib().nsd_workspace_bytes(n), dtype=torch.uint8, device=dev)
 
     def step(ev=None):
         ext_count.zero_()
@@ -111,7 +112,7 @@ def main():
         if ev is not None:
             ev[0].record()
         nsd.dissect_device(frames, desc, mode=args.mode, rec=rec, ext=ext, ext_count=ext_count,
-                           counters=counters, grid=args.grid)
+                           counters=counters, grid=args.grid, workspace=workspace)
         if ev is not None:
             ev[1].record()
         if dist is not None:

@@ -184,6 +184,16 @@ int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32
 		       nsd_rec *d_rec, nsd_ext *d_ext, uint32_t ext_cap,
 		       uint32_t *d_ext_count, uint64_t *d_counters, void *stream);
 
+/* Same, with a caller-provided device workspace of nsd_workspace_bytes(n)
+ * bytes (the compaction queue between the fast and the general pass): no
+ * allocation inside, so the call can be captured in a hipGraph.
+ * nsd_dissect_device uses a library-owned workspace grown on demand. */
+size_t nsd_workspace_bytes(uint32_t n);
+int nsd_dissect_device_ws(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
+			  int linktype, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+			  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+			  void *d_workspace, void *stream);
+
 /* Host-memory batch: stages frames/descriptors to HBM, runs
  * nsd_dissect_device, copies records/ext/counters back.  Synchronous.
  * `counters` may be NULL; `ext` may be NULL when ext_cap == 0. */

@@ -22,7 +22,8 @@
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
 				  int start_id, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
 				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
-				  int grid, hipStream_t stream);
+				  void *d_ws, int grid, hipStream_t stream);
+extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
 
 namespace nsd {
 int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
@@ -84,6 +85,8 @@ struct DevCtx {
 	nsd_ext *ext = nullptr; size_t ext_cap = 0;
 	uint32_t *ext_count = nullptr;
 	uint64_t *counters = nullptr;
+	uint8_t *ws = nullptr; size_t ws_cap = 0;          // queue for entry_batch
+	uint8_t *dev_ws = nullptr; size_t dev_ws_cap = 0;  // nsd_dissect_device's own
 };
 DevCtx g_ctx;
 
@@ -145,21 +148,33 @@ int start_for(int linktype)
 } // namespace
 
 // ---- batch extension ---------------------------------------------------
-extern "C" int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
-				  int linktype, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
-				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
-				  void *stream)
+extern "C" size_t nsd_workspace_bytes(uint32_t n) { return nsd_launch_workspace_bytes(n); }
+
+static int check_device_args(const uint8_t *d_frames, const nsd_desc_t *d_desc, const nsd_rec *d_rec,
+			     const nsd_ext *d_ext, uint32_t ext_cap, const uint32_t *d_ext_count,
+			     const uint64_t *d_counters, int mode)
 {
-	if (n == 0)
-		return NSD_OK;
 	if (!d_frames || !d_desc || !d_rec || !d_ext_count || !d_counters)
 		return NSD_ERR_ARG;
 	if (ext_cap && !d_ext)
 		return NSD_ERR_ARG;
 	if (mode < PRINT_NORM || mode > PRINT_NONE)
 		return NSD_ERR_ARG;
-	int rc = nsd_launch_dissect(d_frames, d_desc, n, start_for(linktype), mode, d_rec, d_ext,
-				    ext_cap, d_ext_count, d_counters, 0, (hipStream_t)stream);
+	return NSD_OK;
+}
+
+extern "C" int nsd_dissect_device_ws(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
+				     int linktype, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+				     uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+				     void *d_workspace, void *stream)
+{
+	if (n == 0)
+		return NSD_OK;
+	int rc = check_device_args(d_frames, d_desc, d_rec, d_ext, ext_cap, d_ext_count, d_counters, mode);
+	if (rc || !d_workspace)
+		return rc ? rc : NSD_ERR_ARG;
+	rc = nsd_launch_dissect(d_frames, d_desc, n, start_for(linktype), mode, d_rec, d_ext, ext_cap,
+				d_ext_count, d_counters, d_workspace, 0, (hipStream_t)stream);
 	return rc ? NSD_ERR_HIP : NSD_OK;
 }
 
@@ -167,14 +182,36 @@ extern "C" int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_d
 extern "C" int nsd_dissect_device_grid(const uint8_t *d_frames, const nsd_desc_t *d_desc,
 				       uint32_t n, int linktype, int mode, nsd_rec *d_rec,
 				       nsd_ext *d_ext, uint32_t ext_cap, uint32_t *d_ext_count,
-				       uint64_t *d_counters, int grid, void *stream)
+				       uint64_t *d_counters, void *d_workspace, int grid, void *stream)
 {
 	if (n == 0)
 		return NSD_OK;
-	if (!d_frames || !d_desc || !d_rec || !d_ext_count || !d_counters)
-		return NSD_ERR_ARG;
-	int rc = nsd_launch_dissect(d_frames, d_desc, n, start_for(linktype), mode, d_rec, d_ext,
-				    ext_cap, d_ext_count, d_counters, grid, (hipStream_t)stream);
+	int rc = check_device_args(d_frames, d_desc, d_rec, d_ext, ext_cap, d_ext_count, d_counters, mode);
+	if (rc || !d_workspace)
+		return rc ? rc : NSD_ERR_ARG;
+	rc = nsd_launch_dissect(d_frames, d_desc, n, start_for(linktype), mode, d_rec, d_ext, ext_cap,
+				d_ext_count, d_counters, d_workspace, grid, (hipStream_t)stream);
+	return rc ? NSD_ERR_HIP : NSD_OK;
+}
+
+// Without a caller workspace the library keeps one per process (allocated on
+// first use and grown on demand: that call is not graph-capturable).
+extern "C" int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
+				  int linktype, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+				  void *stream)
+{
+	if (n == 0)
+		return NSD_OK;
+	int rc = check_device_args(d_frames, d_desc, d_rec, d_ext, ext_cap, d_ext_count, d_counters, mode);
+	if (rc)
+		return rc;
+	DevCtx &c = g_ctx;
+	std::lock_guard<std::mutex> lk(c.mu);
+	if (!grow(c.dev_ws, c.dev_ws_cap, nsd_launch_workspace_bytes(n)))
+		return NSD_ERR_NOMEM;
+	rc = nsd_launch_dissect(d_frames, d_desc, n, start_for(linktype), mode, d_rec, d_ext, ext_cap,
+				d_ext_count, d_counters, c.dev_ws, 0, (hipStream_t)stream);
 	return rc ? NSD_ERR_HIP : NSD_OK;
 }
 
@@ -198,7 +235,8 @@ extern "C" int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
 	if (!ctx_init(c))
 		return NSD_ERR_HIP;
 	if (!grow(c.frames, c.frames_cap, frames_len + NSD_FRAME_PAD) || !grow(c.desc, c.desc_cap, n) ||
-	    !grow(c.rec, c.rec_cap, n) || (ext_cap && !grow(c.ext, c.ext_cap, ext_cap)))
+	    !grow(c.rec, c.rec_cap, n) || (ext_cap && !grow(c.ext, c.ext_cap, ext_cap)) ||
+	    !grow(c.ws, c.ws_cap, nsd_launch_workspace_bytes(n)))
 		return NSD_ERR_NOMEM;
 	hipStream_t s = c.stream;
 	bool ok = hip_ok(hipMemcpyAsync(c.frames, frames, frames_len, hipMemcpyHostToDevice, s), "H2D") &&
@@ -208,7 +246,7 @@ extern "C" int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
 	if (!ok)
 		return NSD_ERR_HIP;
 	if (nsd_launch_dissect(c.frames, c.desc, n, start_for(linktype), mode, c.rec,
-			       ext_cap ? c.ext : nullptr, ext_cap, c.ext_count, c.counters, 0, s))
+			       ext_cap ? c.ext : nullptr, ext_cap, c.ext_count, c.counters, c.ws, 0, s))
 		return NSD_ERR_HIP;
 	uint32_t used = 0;
 	ok = hip_ok(hipMemcpyAsync(rec, c.rec, n * sizeof(nsd_rec), hipMemcpyDeviceToHost, s), "D2H") &&
@@ -312,7 +350,9 @@ extern "C" void dissector_cleanup_all(void)
 	if (!c.init)
 		return;
 	(void)hipFree(c.frames); (void)hipFree(c.desc); (void)hipFree(c.rec); (void)hipFree(c.ext);
-	(void)hipFree(c.ext_count);
+	(void)hipFree(c.ext_count); (void)hipFree(c.ws); (void)hipFree(c.dev_ws);
+	c.ws = c.dev_ws = nullptr;
+	c.ws_cap = c.dev_ws_cap = 0;
 	(void)hipStreamDestroy(c.stream);
 	c.frames = nullptr; c.desc = nullptr; c.rec = nullptr; c.ext = nullptr;
 	c.frames_cap = c.desc_cap = c.rec_cap = c.ext_cap = 0;

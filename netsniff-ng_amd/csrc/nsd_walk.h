@@ -62,6 +62,9 @@ struct WalkOut {
 	bool     need_ext;   // more than 6 layers or a layer start > 510
 	uint32_t slot;       // ext slot (valid when ext_on)
 	bool     ext_on;
+	int      id;         // next ops to run (0 = chain ended)
+	bool     icmp_pend;  // ICMPv4 checksum left to the wave-cooperative pass
+	uint32_t icmp_off, icmp_len;
 };
 
 // Ext spill: the first time a packet needs the ext form it takes a slot and
@@ -131,11 +134,8 @@ __device__ __forceinline__ uint16_t calc_csum(const Src &s, uint32_t off, uint32
 	return (uint16_t)~sum;
 }
 
-// The walk.  MODE is PRINT_NORM or PRINT_LESS (parse semantics differ).
-// Cnt: per-ops counter hook  cnt(id).
-template <int MODE, class Src, class Cnt>
-__device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id,
-				     const ExtSink &es, WalkOut &w, Cnt &&cnt)
+// Walk state initialisation (pkt_alloc: data = head, tail = head + len).
+__device__ __forceinline__ void walk_init(WalkOut &w, uint32_t caplen, int start_id)
 {
 	w.data = 0;
 	w.tail = caplen;
@@ -148,11 +148,44 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 	w.need_ext = false;
 	w.ext_on = false;
 	w.slot = 0;
+	w.id = start_id;
+	w.icmp_pend = false;
+	w.icmp_off = 0;
+	w.icmp_len = 0;
+}
 
-	int id = start_id;
-	while (id) {
-		record_layer(w, id, es);
-		cnt(w.n <= NSD_EXT_MAX_LAYERS ? id : -1);   // the oracle counts the first 64 layers
+// The walk (dissector_main's loop, dissector.c:51-58).  MODE is PRINT_NORM
+// or PRINT_LESS (parse semantics differ).  Runs layers until the chain ends
+// or, when `resumable`, until the next layer starts too close to the end of
+// the source's staged window (returns true: restage at w.data and call again).
+// Cnt: per-ops counter hook cnt(id).
+//
+// FAST (the first-pass kernel): instead of suspending, spilling to the ext
+// table or deferring an ICMP checksum, the walk gives up (returns true) and
+// the packet is queued for the general kernel, which walks it from scratch;
+// counting is left to the caller (from the finished record).
+template <int MODE, bool FAST, class Src, class Cnt>
+__device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSink &es, WalkOut &w,
+				     Cnt &&cnt)
+{
+	(void)caplen;
+	while (w.id) {
+		const int id = w.id;
+		if (s.near_end(w.data, id))
+			return true;
+		if constexpr (FAST) {
+			if (w.n >= NSD_REC_MAX_LAYERS || (w.n >= 1 && w.data > 510))
+				return true;
+			w.chain |= (uint32_t)id << (5 * w.n);
+			if (w.n < 4)
+				w.offA |= (uint64_t)w.data << (16 * w.n);
+			else
+				w.offB |= w.data << (16 * (w.n - 4));
+			w.n++;
+		} else {
+			record_layer(w, id, es);
+			cnt(w.n <= NSD_EXT_MAX_LAYERS ? id : -1);   // the oracle counts the first 64 layers
+		}
 		const uint32_t start = w.data;
 		const uint32_t len = w.tail - w.data;   // pkt_len (pkt_buff.h:36-41)
 		int next = 0;
@@ -310,9 +343,19 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 				w.data = start + 8;
 				if (MODE == PRINT_NORM) {
 					// calc_csum(icmp, pkt_len + 8): the whole (post-trim)
-					// message, odd trailing byte dropped (csum.h:24-27)
-					if (calc_csum(s, start, len >> 1))
-						w.flags |= NSD_F_ICMP_BAD;
+					// message, odd trailing byte dropped (csum.h:24-27).
+					// Short messages inside the staged window are summed
+					// here; longer ones by the whole wave afterwards.
+					if (s.in_window(start, len & ~1u)) {
+						if (calc_csum(s, start, len >> 1))
+							w.flags |= NSD_F_ICMP_BAD;
+					} else if constexpr (FAST) {
+						return true;
+					} else {
+						w.icmp_pend = true;
+						w.icmp_off = start;
+						w.icmp_len = len;
+					}
 				}
 			}
 			break;
@@ -339,8 +382,9 @@ __device__ __forceinline__ void walk(const Src &s, uint32_t caplen, int start_id
 			w.data = start;
 			break;
 		}
-		id = next;
+		w.id = next;
 	}
+	return false;
 }
 
 } // namespace nsd

@@ -36,7 +36,7 @@ OPS_NAMES = ["invalid", "ethernet", "vlan", "QinQ", "mpls_uc", "arp", "lldp", "i
 # every entry point declared in include/netsniff_dissect.h
 ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup_all",
                "dissector_set_print_type", "nsd_dissect_device", "dissector_entry_batch",
-               "nsd_format_packet", "nsd_lookup_init", "nsd_lookup_cleanup", "nsd_tprintf_wrap",
+               "nsd_workspace_bytes", "nsd_dissect_device_ws", "nsd_format_packet", "nsd_lookup_init", "nsd_lookup_cleanup", "nsd_tprintf_wrap",
                "nsd_version", "nsd_device_count"]
 
 _lib = None
@@ -61,7 +61,12 @@ def lib():
         L.nsd_dissect_device.argtypes = [_vp, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp, _vp]
         L.nsd_dissect_device_grid.restype = _int
         L.nsd_dissect_device_grid.argtypes = [_vp, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp,
-                                              _int, _vp]
+                                              _vp, _int, _vp]
+        L.nsd_dissect_device_ws.restype = _int
+        L.nsd_dissect_device_ws.argtypes = [_vp, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp,
+                                            _vp, _vp]
+        L.nsd_workspace_bytes.restype = _sz
+        L.nsd_workspace_bytes.argtypes = [_u32]
         L.dissector_entry_batch.restype = _int
         L.dissector_entry_batch.argtypes = [_vp, _sz, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp]
         L.nsd_format_packet.restype = ctypes.c_long
@@ -92,7 +97,7 @@ def _check(rc, what):
 
 
 def dissect_device(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, rec=None, ext=None,
-                   ext_count=None, counters=None, grid=0, stream=None):
+                   ext_count=None, counters=None, grid=0, stream=None, workspace=None):
     """Walk a device-resident batch.  frames: uint8 cuda tensor (padded by
     FRAME_PAD bytes), desc: int64/uint64 cuda tensor (packed descriptors).
     Returns (rec u8[n*16], ext u8[cap*200], ext_count i32[1], counters i64[64])
@@ -112,14 +117,16 @@ def dissect_device(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, rec=
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
     L = lib()
+    if workspace is None:
+        workspace = torch.empty(L.nsd_workspace_bytes(n), dtype=torch.uint8, device=dev)
     if grid:
         rc = L.nsd_dissect_device_grid(frames.data_ptr(), desc.data_ptr(), n, linktype, mode,
                                        rec.data_ptr(), ext.data_ptr(), ext_cap, ext_count.data_ptr(),
-                                       counters.data_ptr(), grid, stream)
+                                       counters.data_ptr(), workspace.data_ptr(), grid, stream)
     else:
-        rc = L.nsd_dissect_device(frames.data_ptr(), desc.data_ptr(), n, linktype, mode,
-                                  rec.data_ptr(), ext.data_ptr(), ext_cap, ext_count.data_ptr(),
-                                  counters.data_ptr(), stream)
+        rc = L.nsd_dissect_device_ws(frames.data_ptr(), desc.data_ptr(), n, linktype, mode,
+                                     rec.data_ptr(), ext.data_ptr(), ext_cap, ext_count.data_ptr(),
+                                     counters.data_ptr(), workspace.data_ptr(), stream)
     _check(rc, "nsd_dissect_device")
     return rec, ext, ext_count, counters
 
