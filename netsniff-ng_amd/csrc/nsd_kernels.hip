@@ -1,23 +1,28 @@
 // nsd_kernels.hip - CDNA4 (gfx950) kernels for the netsniff-ng dissector chain.
 //
 // One lane walks one packet (nsd_walk.h).  Layout in HBM:
-//   frames  : one byte buffer, frames at arbitrary offsets (16-byte aligned
-//             frames take the dwordx4 fast path)
+//   frames  : one byte buffer, frames at arbitrary offsets
 //   desc    : u64 per packet (bits 0..39 offset, 40..63 caplen)
 //   rec     : 16-byte chain record per packet (nsd_rec), one dwordx4 store per
 //             lane -> 1 KiB contiguous per wave
-//   ext     : overflow records for deep chains, slots by atomic counter
+//   ext     : overflow records for deep chains, slots by wave-aggregated atomic
 //   counters: u64[64] per-ops / flag counts
 //
-// Header bytes are staged through LDS: each wave copies the first WIN bytes of
-// its 64 packets into an LDS window (16-byte chunks, WIN/16 consecutive lanes
-// per packet so each packet's header is read as one contiguous segment), and
-// the walk reads the window; bytes beyond WIN (deep IPv6 chains, long ICMP
-// payloads) come from global memory.  Bytes >= caplen read as zero.
+// Header windows are staged through LDS in "aligned coordinates": a frame at
+// byte offset `off` is read from A = off & ~15 in whole 16-byte chunks (every
+// load a global_load_dwordx4, whatever the frame's alignment; AF_PACKET rings
+// put the MAC header at 2 mod 16), and frame byte o sits at window position
+// o + m, m = off & 15.  Window bytes at frame offsets >= caplen are zeroed.
+// The window is stored transposed by dword: dword j of lane l's window lives
+// at win[j * 64 + l], so 64 lanes reading the same header offset hit 64
+// consecutive LDS dwords.
 //
-// Counting is wave-aggregated: per layer step the active lanes are grouped by
-// ops id with ballot / readfirstlane, one lane adds the popcount into the
-// block's LDS counters, and each block adds its counters to HBM once.
+// Pass 1 (dissect_fast) finishes every packet whose chain resolves inside its
+// first 64 bytes, with the next tile's chunks and the tile after next's
+// descriptors in flight while the current tile is walked from LDS only.  The
+// rest is compacted into a queue (ballot + one atomic per wave + mbcnt) for
+// pass 2 (dissect_general): per-lane window restaging at each lane's cursor,
+// ext spill, per-lane ICMPv4 payload checksums.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,29 +32,55 @@ namespace nsd {
 
 constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
+constexpr int WIN = 64;          // bytes per staged window
+constexpr int CPP = WIN / 16;    // 16-byte chunks per window
 
-// LDS window + global fallback.  The window holds bytes [0, WIN) of the
-// frame with bytes >= caplen already zeroed.  Stored transposed by dword:
-// dword j of lane l's packet lives at win[j * 64 + l], so the 64 lanes of a
-// wave reading the same header offset hit 64 consecutive dwords (no bank
-// conflicts).
-template <int WIN>
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m)
+{
+	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
+{
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		v += __shfl_xor(v, o, 64);
+	return v;
+}
+
+// Byte source over an LDS window (aligned coordinates, see top).
+// FAST: bytes outside the window are not fetched; the source records the
+// miss and the walk gives the packet up to pass 2.  Otherwise they come from
+// HBM (zero past caplen).
+template <bool FAST>
 struct LSrc {
-	const uint32_t *win;   // this wave's window base + lane
-	const uint8_t *p;      // frame in HBM (fallback outside the window)
+	const uint32_t *win;     // this wave's window array + lane
+	const uint8_t *lay3t;    // LDS copy of eth_lay3
+	const uint8_t *p;        // frame in HBM
 	uint32_t caplen;
-	uint32_t base;         // frame offset of window byte 0 (multiple of 16)
+	uint32_t m;              // off & 15
+	uint32_t wb;             // aligned position of window byte 0 (multiple of 16)
+	mutable bool miss;
+
 	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return win[j * 64]; }
+	__device__ __forceinline__ int lay3(uint32_t key) const { return lay3t[key & 255]; }
+	__device__ __forceinline__ bool missed() const { return miss; }
 	__device__ __forceinline__ uint8_t b(uint32_t o) const
 	{
-		const uint32_t r = o - base;
+		const uint32_t r = o + m - wb;
 		if (r < WIN)
 			return (uint8_t)(dw(r >> 2) >> ((r & 3) * 8));
-		return o < caplen ? p[o] : 0;
+		if constexpr (FAST) {
+			if (o < caplen)
+				miss = true;
+			return 0;
+		} else {
+			return o < caplen ? p[o] : 0;
+		}
 	}
 	__device__ __forceinline__ uint16_t le16(uint32_t o) const
 	{
-		const uint32_t r = o - base;
+		const uint32_t r = o + m - wb;
 		if (r + 1 < WIN && (r & 3) != 3)
 			return (uint16_t)(dw(r >> 2) >> ((r & 3) * 8));
 		return (uint16_t)(b(o) | b(o + 1) << 8);
@@ -60,11 +91,12 @@ struct LSrc {
 	}
 	__device__ __forceinline__ bool in_window(uint32_t o, uint32_t nbytes) const
 	{
-		return o >= base && o + nbytes <= base + WIN;
+		const uint32_t r = o + m - wb;
+		return r < WIN && r + nbytes <= WIN;
 	}
-	// the next layer would read past the staged window (bytes a layer's
-	// process() inspects, counted from its start; longer reads such as
-	// IPv4 options or routing addresses use the global fallback)
+	// the next layer would read past the staged window (bytes its process()
+	// inspects, from its start; longer reads such as IPv4 options use the
+	// fallback)
 	__device__ __forceinline__ bool near_end(uint32_t o, int id) const
 	{
 		uint32_t need;
@@ -78,15 +110,16 @@ struct LSrc {
 		case NSD_OPS_IP_AUTH: case NSD_OPS_IPV6_MOBILITY: case NSD_OPS_ICMPV6: need = 4; break;
 		default: need = 0;
 		}
-		return need && o < caplen && o + need > base + WIN;
+		return need && o < caplen && o + m + need > wb + WIN;
 	}
 	// sum of `nwords` little-endian u16 words from `o` (csum.h:16-17)
 	__device__ __forceinline__ uint32_t sum16(uint32_t o, uint32_t nwords) const
 	{
 		uint32_t sum = 0;
-		if (!(o & 1) && in_window(o, 2 * nwords)) {
-			uint32_t j = (o - base) >> 2, k = nwords;
-			if ((o & 2) && k) { sum += dw(j) >> 16; j++; k--; }
+		const uint32_t r = o + m - wb;
+		if (!(r & 1) && in_window(o, 2 * nwords)) {
+			uint32_t j = r >> 2, k = nwords;
+			if ((r & 2) && k) { sum += dw(j) >> 16; j++; k--; }
 			for (; k >= 2; k -= 2, j++) { const uint32_t v = dw(j); sum += (v & 0xFFFF) + (v >> 16); }
 			if (k) sum += dw(j) & 0xFFFF;
 			return sum;
@@ -97,10 +130,8 @@ struct LSrc {
 	}
 };
 
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
-
-// Wave-aggregated counting into the block's LDS counters: the active lanes
-// are grouped by value; the group leader adds the group's size.
+// Wave-aggregated per-layer counting into the block's LDS counters (pass 2):
+// active lanes are grouped by ops id, the group leader adds its size.
 struct WaveCnt {
 	unsigned long long *s_cnt;
 	__device__ __forceinline__ void operator()(int id) const
@@ -113,7 +144,7 @@ struct WaveCnt {
 			const int leader = __ffsll((unsigned long long)pend) - 1;
 			const int lid = __shfl(my, leader, 64);
 			const uint64_t m = __ballot(my == lid);
-			if (lane_id() == leader)
+			if ((int)__lane_id() == leader)
 				atomicAdd(&s_cnt[NSD_CNT_OPS + lid], (unsigned long long)__popcll(m));
 			if (my == lid)
 				my = -1;
@@ -121,111 +152,113 @@ struct WaveCnt {
 	}
 };
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
-{
-#pragma unroll
-	for (int o = 32; o > 0; o >>= 1)
-		v += __shfl_xor(v, o, 64);
-	return v;
-}
+// ---- staging ---------------------------------------------------------------
+// Chunk r of the wave: lane (q * CPP + c) % 64 in round (q * CPP + c) / 64
+// loads chunk c of packet q's window, so the CPP chunks of one packet are
+// read by consecutive lanes as one contiguous, 16-byte aligned segment.
 
-// Stage WIN bytes of each participating packet of the wave into LDS, from
-// frame offset my_base (a multiple of 16).  Chunk c (16 bytes at window
-// offset 16c) of packet q is loaded by lane (q * CPP + c) % 64 in round
-// (q * CPP + c) / 64, CPP = WIN / 16: the CPP chunks of one packet are read
-// by consecutive lanes as one contiguous segment.  Bytes at frame offsets
-// >= caplen are written as zero.
-template <int WIN>
-__device__ __forceinline__ void stage(uint32_t *wwin, const uint8_t *frames, uint64_t my_off,
-				      uint32_t my_cap, uint32_t my_base, bool my_part, int lane)
+struct Chunks {
+	uint4 v[CPP];
+};
+
+// issue the loads (no wait): chunk c of lane q's window = aligned bytes
+// [A_q + wb_q + 16c, +16); skipped when the whole chunk is past caplen
+__device__ __forceinline__ void stage_load(Chunks &ch, const uint8_t *frames, uint64_t my_off,
+					   uint32_t my_cap, uint32_t my_wb, bool my_part, int lane)
 {
-	constexpr int CPP = WIN / 16;
 #pragma unroll
 	for (int r = 0; r < CPP; r++) {
 		const int t = r * 64 + lane;
-		const int q = t / CPP;
-		const int c = t % CPP;
+		const int q = t / CPP, c = t % CPP;
 		const uint64_t off = __shfl(my_off, q, 64);
 		const uint32_t cap = __shfl(my_cap, q, 64);
-		const uint32_t wb = __shfl(my_base, q, 64);
+		const uint32_t wb = __shfl(my_wb, q, 64);
+		const bool part = __shfl((int)my_part, q, 64);
+		const uint32_t pos = wb + 16u * c;                 // aligned position of the chunk
+		const uint32_t m = (uint32_t)off & 15;
+		if (part && pos < cap + m)
+			ch.v[r] = *(const uint4 *)(frames + (off & ~15ull) + pos);
+		else
+			ch.v[r] = make_uint4(0, 0, 0, 0);
+	}
+}
+
+// write the chunks to the transposed window, zeroing bytes at frame offsets
+// >= caplen (aligned position >= caplen + m)
+__device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks &ch, uint64_t my_off,
+					    uint32_t my_cap, uint32_t my_wb, bool my_part, int lane)
+{
+#pragma unroll
+	for (int r = 0; r < CPP; r++) {
+		const int t = r * 64 + lane;
+		const int q = t / CPP, c = t % CPP;
+		const uint32_t m = (uint32_t)__shfl((uint32_t)my_off, q, 64) & 15;
+		const uint32_t cap = __shfl(my_cap, q, 64);
+		const uint32_t wb = __shfl(my_wb, q, 64);
 		const bool part = __shfl((int)my_part, q, 64);
 		if (!part)
 			continue;
-		const uint32_t fo = wb + (uint32_t)c * 16;   // frame offset of this chunk
-		uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-		if (fo < cap) {
-			const uint64_t a = off + fo;
-			if ((a & 15) == 0) {
-				const uint4 v = *(const uint4 *)(frames + a);
-				w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
-			} else {
-				const uint32_t mis = (uint32_t)(a & 3);
-				const uint32_t *src = (const uint32_t *)(frames + (a - mis));
-				uint32_t d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
-				if (mis) {
-					const uint32_t d4 = src[4], sh = mis * 8;
-					d0 = (d0 >> sh) | (d1 << (32 - sh));
-					d1 = (d1 >> sh) | (d2 << (32 - sh));
-					d2 = (d2 >> sh) | (d3 << (32 - sh));
-					d3 = (d3 >> sh) | (d4 << (32 - sh));
-				}
-				w0 = d0; w1 = d1; w2 = d2; w3 = d3;
-			}
-			if (fo + 16 > cap) {   // zero bytes at frame offsets >= caplen
-				const uint32_t keep = cap - fo;   // 1..15 bytes
-				auto mask = [&](uint32_t &w, uint32_t bo) {
-					if (bo >= keep) w = 0;
-					else if (bo + 4 > keep) w &= (1u << ((keep - bo) * 8)) - 1u;
-				};
-				mask(w0, 0); mask(w1, 4); mask(w2, 8); mask(w3, 12);
+		const uint32_t pos = wb + 16u * c;
+		const uint32_t lim = cap + m;                      // first aligned position past the frame
+		uint32_t w[4] = { ch.v[r].x, ch.v[r].y, ch.v[r].z, ch.v[r].w };
+		if (pos + 16 > lim) {
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				const uint32_t bp = pos + 4 * j;
+				if (bp >= lim)
+					w[j] = 0;
+				else if (bp + 4 > lim)
+					w[j] &= (1u << ((lim - bp) * 8)) - 1u;
 			}
 		}
 		uint32_t *dst = wwin + (c * 4) * 64 + q;
-		dst[0] = w0;
-		dst[64] = w1;
-		dst[128] = w2;
-		dst[192] = w3;
+		dst[0] = w[0];
+		dst[64] = w[1];
+		dst[128] = w[2];
+		dst[192] = w[3];
 	}
 }
 
-// Wave-cooperative ICMPv4 checksum (calc_csum over [a, a + nbytes), nbytes
-// even, csum.h:24-27): the wave reads the message as consecutive dwords
-// (lane l takes dwords l, l+64, ...: 256 contiguous bytes per load
-// instruction).  Each byte is weighted by the parity of its distance from `a`
-// (1 for the low byte of an LE word, 256 for the high byte), which makes the
-// sum independent of the message's alignment.  `a` is wave-uniform.  Returns
-// the folded one's-complement result in every lane.
-__device__ __forceinline__ uint16_t wave_csum(const uint8_t *frames, uint64_t a, uint32_t nbytes, int lane)
+__device__ __forceinline__ void wave_sync_lds()
 {
-	const uint32_t alo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-	const uint32_t ahi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-	const uint64_t au = ((uint64_t)ahi << 32) | alo;
-	const uint32_t *p = (const uint32_t *)(frames + (au & ~3ull));
-	const uint32_t s0 = alo & 3, endb = s0 + nbytes;   // byte range [s0, endb) of p
-	const bool odd = alo & 1;
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Per-lane ICMPv4 checksum over [a, a + nbytes) (nbytes even, csum.h:24-27):
+// 16-byte aligned loads; each byte is weighted by the parity of its distance
+// from `a` (1 for the low byte of an LE word, 256 for the high byte), which
+// makes the sum independent of the message's alignment.
+__device__ __forceinline__ uint16_t lane_csum(const uint8_t *frames, uint64_t a, uint32_t nbytes)
+{
+	const uint4 *p = (const uint4 *)(frames + (a & ~15ull));
+	const uint32_t s0 = (uint32_t)(a & 15), endb = s0 + nbytes;
+	const bool odd = a & 1;
 	uint32_t sum = 0;
-	for (uint32_t j = lane; 4 * j < endb; j += 64) {
-		uint32_t x = p[j];
-		const uint32_t lo = 4 * j;
+	auto add = [&](uint32_t x, uint32_t lo) {
+		if (lo + 4 <= s0 || lo >= endb)
+			return;
 		if (lo < s0)
-			x &= 0xFFFFFFFFu << (8 * s0);
+			x &= 0xFFFFFFFFu << (8 * (s0 - lo));
 		if (lo + 4 > endb)
 			x &= 0xFFFFFFFFu >> (8 * (lo + 4 - endb));
-		const uint32_t ev = (x & 0x00FF00FFu), od = (x >> 8) & 0x00FF00FFu;
+		const uint32_t ev = x & 0x00FF00FFu, od = (x >> 8) & 0x00FF00FFu;
 		const uint32_t e2 = (ev & 0xFFFF) + (ev >> 16), o2 = (od & 0xFFFF) + (od >> 16);
 		sum += odd ? (e2 << 8) + o2 : e2 + (o2 << 8);
+	};
+	const uint32_t nchunk = (endb + 15) >> 4;
+#pragma unroll 4
+	for (uint32_t j = 0; j < nchunk; j++) {
+		const uint4 v = p[j];
+		add(v.x, 16 * j);
+		add(v.y, 16 * j + 4);
+		add(v.z, 16 * j + 8);
+		add(v.w, 16 * j + 12);
 	}
-#pragma unroll
-	for (int o = 32; o > 0; o >>= 1)
-		sum += __shfl_xor(sum, o, 64);
 	sum = (sum >> 16) + (sum & 0xffff);
 	sum += (sum >> 16);
 	return (uint16_t)~sum;
-}
-
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m)
-{
-	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
 // record words of a finished walk (layout of nsd_rec)
@@ -281,6 +314,15 @@ struct FlagCnt {
 	}
 };
 
+__device__ __forceinline__ void block_init(unsigned long long *s_cnt, uint8_t *s_lay3)
+{
+	for (int k = threadIdx.x; k < NSD_NCOUNTERS; k += BLOCK)
+		s_cnt[k] = 0;
+	for (int k = threadIdx.x; k < 256; k += BLOCK)
+		s_lay3[k] = c_lay3[k];
+	__syncthreads();
+}
+
 __device__ __forceinline__ void block_flush(unsigned long long *s_cnt, unsigned long long *counters)
 {
 	__syncthreads();
@@ -289,73 +331,93 @@ __device__ __forceinline__ void block_flush(unsigned long long *s_cnt, unsigned 
 			atomicAdd(&counters[k], s_cnt[k]);
 }
 
-// Pass 1: every packet whose chain resolves inside its first WIN bytes
-// (<= 6 layers, checksummed bytes inside the window) is finished here; the
-// others are appended to `queue` (wave-aggregated: one atomic per wave, slots
-// by mbcnt prefix) for dissect_general.
-template <int MODE, int WIN>
+// ---- pass 1 ------------------------------------------------------------------
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void dissect_fast(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n,
 	int start_id, uint4 *__restrict__ rec, unsigned long long *__restrict__ counters,
-	uint32_t *__restrict__ queue, uint32_t *__restrict__ qcount)
+	uint32_t *__restrict__ queue, uint32_t region, uint32_t *__restrict__ qblk)
 {
 	__shared__ uint32_t s_win[WAVES][(WIN / 4) * 64];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
+	__shared__ uint8_t s_lay3[256];
+	__shared__ uint32_t s_qn;
 
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
-	for (int k = threadIdx.x; k < NSD_NCOUNTERS; k += BLOCK)
-		s_cnt[k] = 0;
-	__syncthreads();
+	if (threadIdx.x == 0)
+		s_qn = 0;
+	block_init(s_cnt, s_lay3);
 
-	const ExtSink es{ nullptr, 0, nullptr };
 	const uint32_t stride = gridDim.x * BLOCK;
+	uint32_t *const bq = queue + (size_t)blockIdx.x * region;   // this block's queue region
 	FlagCnt fc;
+	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
 
-	for (uint32_t base = blockIdx.x * BLOCK + wv * 64; base < n; base += stride) {
-		const uint32_t i = base + lane;
-		const bool valid = i < n;
-		const uint64_t d = valid ? desc[i] : 0;
-		const uint64_t off = NSD_DESC_OFF(d);
-		const uint32_t caplen = NSD_DESC_CAPLEN(d);
-
-		if (MODE != PRINT_NORM && MODE != PRINT_LESS) {
-			// every process() is NULL: no chain (dissector.c:51-53)
-			if (valid) {
+	if (MODE != PRINT_NORM && MODE != PRINT_LESS) {
+		// every process() is NULL: no chain (dissector.c:51-53)
+		for (; base < n; base += stride) {
+			const uint32_t i = base + lane;
+			if (i < n) {
+				const uint32_t caplen = NSD_DESC_CAPLEN(desc[i]);
 				rec[i] = make_uint4(0, caplen << 16, 0, 0);
 				fc.pkts++;
 				fc.bytes += caplen;
 			}
-			continue;
 		}
+		fc.flush(s_cnt, lane);
+		block_flush(s_cnt, counters);
+		if (threadIdx.x == 0)
+			qblk[blockIdx.x] = 0;
+		return;
+	}
 
-		stage<WIN>(&s_win[wv][0], frames, off, caplen, 0, valid, lane);
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-		__builtin_amdgcn_wave_barrier();
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
+	// descriptors are in flight
+	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
+	uint64_t d1 = (base + stride + lane < n) ? desc[base + stride + lane] : 0;
+	Chunks ch;
+	stage_load(ch, frames, NSD_DESC_OFF(d0), NSD_DESC_CAPLEN(d0), 0, base + lane < n, lane);
+
+	for (; base < n; base += stride) {
+		const uint32_t i = base + lane;
+		const bool valid = i < n;
+		const uint64_t off = NSD_DESC_OFF(d0);
+		const uint32_t caplen = NSD_DESC_CAPLEN(d0);
+
+		stage_write(&s_win[wv][0], ch, off, caplen, 0, valid, lane);
+		// prefetch: descriptors of tile t+2, chunks of tile t+1
+		const uint32_t b2 = base + 2 * stride;
+		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
+		const uint32_t b1 = base + stride;
+		if (b1 < n)
+			stage_load(ch, frames, NSD_DESC_OFF(d1), NSD_DESC_CAPLEN(d1), 0, b1 + lane < n, lane);
+		wave_sync_lds();
+
 		WalkOut w;
 		walk_init(w, caplen, valid ? start_id : 0);
 		bool deferred = false;
 		if (valid) {
-			const LSrc<WIN> src{ &s_win[wv][lane], frames + off, caplen, 0 };
-			deferred = walk<MODE, true>(src, caplen, es, w, 0);
+			const LSrc<true> src{ &s_win[wv][lane], s_lay3, frames + off, caplen,
+					      (uint32_t)off & 15, 0, false };
+			deferred = walk<MODE, true>(src, caplen, ExtSink{ nullptr, 0, nullptr }, w, 0);
 		}
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-		__builtin_amdgcn_wave_barrier();
+		wave_sync_lds();
 
 		const uint64_t dm = __ballot(deferred);
 		if (dm) {
+			const int leader = __ffsll((unsigned long long)dm) - 1;
 			uint32_t qb = 0;
-			if (lane == __ffsll((unsigned long long)dm) - 1)
-				qb = atomicAdd(qcount, (uint32_t)__popcll(dm));
-			qb = __shfl(qb, __ffsll((unsigned long long)dm) - 1, 64);
+			if (lane == leader)
+				qb = atomicAdd(&s_qn, (uint32_t)__popcll(dm));   // LDS: no global contention
+			qb = __shfl(qb, leader, 64);
 			if (deferred)
-				queue[qb + lanes_below(dm)] = i;
+				bq[qb + lanes_below(dm)] = i;
 		}
 		const bool done = valid && !deferred;
-		// per-ops counts from the finished chains, grouped by chain value
+		// per-ops counts from the finished chains, grouped by chain word
+		// (ids are >= 1, so equal chain words imply equal layer counts)
 		{
-			// ids are >= 1, so equal chain words imply equal layer counts
 			uint32_t key = done ? w.chain : 0xFFFFFFFFu;
 			for (;;) {
 				const uint64_t pend = __ballot(key != 0xFFFFFFFFu);
@@ -367,7 +429,8 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 				if (lane == leader) {
 					const uint32_t cnt = (uint32_t)__popcll(m);
 					for (uint32_t k = 0, nl = w.n; k < nl; k++)
-						atomicAdd(&s_cnt[NSD_CNT_OPS + ((lk >> (5 * k)) & 31)], (unsigned long long)cnt);
+						atomicAdd(&s_cnt[NSD_CNT_OPS + ((lk >> (5 * k)) & 31)],
+							  (unsigned long long)cnt);
 				}
 				if (key == lk)
 					key = 0xFFFFFFFFu;
@@ -377,79 +440,73 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 			rec[i] = pack_record(w);
 			fc.add(w, caplen);
 		}
+		d0 = d1;
+		d1 = d2;
 	}
 	fc.flush(s_cnt, lane);
 	block_flush(s_cnt, counters);
+	if (threadIdx.x == 0)
+		qblk[blockIdx.x] = s_qn;   // block_flush's barrier ordered every append before this
 }
 
-// Pass 2: the queued packets, one lane each (compacted), walked from scratch
-// with per-lane window restaging, ext spill and wave-cooperative ICMPv4
-// checksums.
-template <int MODE, int WIN>
+// ---- pass 2 ------------------------------------------------------------------
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void dissect_general(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, int start_id,
 	uint4 *__restrict__ rec, nsd_ext *__restrict__ ext, uint32_t ext_cap,
 	uint32_t *__restrict__ ext_count, unsigned long long *__restrict__ counters,
-	const uint32_t *__restrict__ queue, const uint32_t *__restrict__ qcount)
+	const uint32_t *__restrict__ queue, uint32_t region, const uint32_t *__restrict__ qblk)
 {
 	__shared__ uint32_t s_win[WAVES][(WIN / 4) * 64];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
+	__shared__ uint8_t s_lay3[256];
 
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
-	for (int k = threadIdx.x; k < NSD_NCOUNTERS; k += BLOCK)
-		s_cnt[k] = 0;
-	__syncthreads();
+	block_init(s_cnt, s_lay3);
 
-	const uint32_t nq = *qcount;
+	// block b drains the queue region pass 1's block b filled
+	const uint32_t nq = qblk[blockIdx.x];
+	const uint32_t *const bq = queue + (size_t)blockIdx.x * region;
 	const WaveCnt wc{ s_cnt };
 	const ExtSink es{ ext, ext_cap, ext_count };
-	const uint32_t stride = gridDim.x * BLOCK;
 	FlagCnt fc;
 
-	for (uint32_t base = blockIdx.x * BLOCK + wv * 64; base < nq; base += stride) {
+	for (uint32_t base = wv * 64; base < nq; base += BLOCK) {
 		const uint32_t k = base + lane;
 		const bool valid = k < nq;
-		const uint32_t i = valid ? queue[k] : 0;
+		const uint32_t i = valid ? bq[k] : 0;
 		const uint64_t d = valid ? desc[i] : 0;
 		const uint64_t off = NSD_DESC_OFF(d);
 		const uint32_t caplen = NSD_DESC_CAPLEN(d);
+		const uint32_t m = (uint32_t)off & 15;
 
 		WalkOut w;
 		walk_init(w, caplen, valid ? start_id : 0);
-		uint32_t wbase = 0;
+		uint32_t wb = 0;
 		bool part = valid;
 		// lanes whose next header lies past their window suspend; the wave
 		// restages those windows at the lanes' cursors and resumes them
 		for (;;) {
-			stage<WIN>(&s_win[wv][0], frames, off, caplen, wbase, part, lane);
-			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-			__builtin_amdgcn_wave_barrier();
-			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			Chunks ch;
+			stage_load(ch, frames, off, caplen, wb, part, lane);
+			stage_write(&s_win[wv][0], ch, off, caplen, wb, part, lane);
+			wave_sync_lds();
 			bool susp = false;
 			if (part) {
-				const LSrc<WIN> src{ &s_win[wv][lane], frames + off, caplen, wbase };
+				const LSrc<false> src{ &s_win[wv][lane], s_lay3, frames + off, caplen, m, wb, false };
 				susp = walk<MODE, false>(src, caplen, es, w, wc);
 			}
-			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-			__builtin_amdgcn_wave_barrier();
+			wave_sync_lds();
 			if (!__ballot(susp))
 				break;
 			part = susp;
 			if (susp)
-				wbase = w.data & ~15u;
+				wb = (w.data + m) & ~15u;
 		}
-		if (MODE == PRINT_NORM) {
-			uint64_t pend = __ballot(w.icmp_pend);
-			while (pend) {
-				const int l = __ffsll((unsigned long long)pend) - 1;
-				pend &= pend - 1;
-				const uint64_t a = __shfl(off, l, 64) + __shfl(w.icmp_off, l, 64);
-				const uint32_t nb = __shfl(w.icmp_len, l, 64) & ~1u;
-				const uint16_t cs = wave_csum(frames, a, nb, lane);
-				if (lane == l && cs)
-					w.flags |= NSD_F_ICMP_BAD;
-			}
+		if (MODE == PRINT_NORM && w.icmp_pend) {
+			if (lane_csum(frames, off + w.icmp_off, w.icmp_len & ~1u))
+				w.flags |= NSD_F_ICMP_BAD;
 		}
 		if (!valid)
 			continue;
@@ -468,8 +525,23 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 } // namespace nsd
 
 // ---- launchers (C ABI, called by nsd_host.cpp) ------------------------------
-// workspace: [0, 64) queue counter (zeroed here), [64, 64 + 4n) queue
-extern "C" size_t nsd_launch_workspace_bytes(uint32_t n) { return 64 + 4 * (size_t)n; }
+// Pass 1 runs a persistent grid of at most NSD_MAX_GRID blocks; block b owns
+// queue region b (room for every packet it visits) and writes its deferred
+// count to qblk[b]; pass 2 runs the same grid, block b draining region b.
+// workspace: qblk[NSD_MAX_GRID] u32, then the regions.
+constexpr uint32_t NSD_MAX_GRID = 4096;
+
+static uint32_t region_for(uint32_t n, uint32_t blocks)
+{
+	const uint64_t stride = (uint64_t)blocks * nsd::BLOCK;
+	return (uint32_t)(((n + stride - 1) / stride) * nsd::BLOCK);
+}
+
+extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
+{
+	// worst case over grids: sum of regions <= n + blocks * BLOCK
+	return 4 * (size_t)NSD_MAX_GRID + 4 * ((size_t)n + (size_t)NSD_MAX_GRID * nsd::BLOCK);
+}
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
 				  int start_id, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
@@ -490,32 +562,34 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	uint32_t blocks = (waves + WAVES - 1) / WAVES;
 	// persistent grid: enough resident blocks to fill every CU, the rest
 	// grid-strides (counters then cost one flush per block)
-	const uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)s_cus * 8;
+	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)s_cus * 8;
+	if (cap_blocks > NSD_MAX_GRID)
+		cap_blocks = NSD_MAX_GRID;
 	if (blocks > cap_blocks)
 		blocks = cap_blocks;
-	const uint32_t gblocks = (uint32_t)s_cus * 4;
+	const uint32_t region = region_for(n, blocks);
 	unsigned long long *cnt = (unsigned long long *)d_counters;
 	uint4 *rec = (uint4 *)d_rec;
-	uint32_t *qcount = (uint32_t *)d_ws;
-	uint32_t *queue = (uint32_t *)((uint8_t *)d_ws + 64);
-	if (hipMemsetAsync(qcount, 0, 64, stream) != hipSuccess)
-		return -2;
+	uint32_t *qblk = (uint32_t *)d_ws;
+	uint32_t *queue = qblk + NSD_MAX_GRID;
 	switch (mode) {
 	case PRINT_NORM:
-		hipLaunchKernelGGL((dissect_fast<PRINT_NORM, 64>), dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, qcount);
-		hipLaunchKernelGGL((dissect_general<PRINT_NORM, 64>), dim3(gblocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue, qcount);
+		hipLaunchKernelGGL(dissect_fast<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk);
+		hipLaunchKernelGGL(dissect_general<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
+				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
+				   region, qblk);
 		break;
 	case PRINT_LESS:
-		hipLaunchKernelGGL((dissect_fast<PRINT_LESS, 64>), dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, qcount);
-		hipLaunchKernelGGL((dissect_general<PRINT_LESS, 64>), dim3(gblocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue, qcount);
+		hipLaunchKernelGGL(dissect_fast<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk);
+		hipLaunchKernelGGL(dissect_general<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
+				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
+				   region, qblk);
 		break;
 	default:
-		hipLaunchKernelGGL((dissect_fast<PRINT_HEX, 64>), dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, qcount);
+		hipLaunchKernelGGL(dissect_fast<PRINT_HEX>, dim3(blocks), dim3(BLOCK), 0, stream,
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk);
 		break;
 	}
 	return hipGetLastError() == hipSuccess ? 0 : -2;

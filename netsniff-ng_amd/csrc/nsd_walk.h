@@ -48,7 +48,9 @@ __constant__ uint8_t c_lay3[256] = {
 	/* 128 */ 0, 0, 0, 0, 0, 0, 0, NSD_OPS_IPV6_MOBILITY, 0, 0, 0, 0, 0, 0, 0, 0,
 };
 
-__device__ __forceinline__ int lay3(uint32_t key) { return c_lay3[key & 255]; }
+// the walk looks eth_lay3 up through its byte source (s.lay3(key)), which
+// serves it from an LDS copy of c_lay3: a per-lane constant-memory read would
+// be a vector-memory load inside the walk
 
 // Per-packet walk output (kept in registers).
 struct WalkOut {
@@ -94,8 +96,20 @@ __device__ __forceinline__ void record_layer(WalkOut &w, int id, const ExtSink &
 	} else {
 		w.need_ext = true;
 	}
-	if (w.need_ext && !w.ext_on && !(w.flags & NSD_F_OVERFLOW)) {
-		uint32_t s = atomicAdd(es.count, 1u);
+	// ext slot: one atomic per group of lanes reaching this point together
+	// (ballot / shfl / mbcnt over the active lanes), not one per lane
+	const bool want = w.need_ext && !w.ext_on && !(w.flags & NSD_F_OVERFLOW);
+	const uint64_t wm = __ballot(want);
+	if (wm) {
+		const int leader = __ffsll((unsigned long long)wm) - 1;
+		uint32_t sb = 0;
+		if ((int)__lane_id() == leader)
+			sb = atomicAdd(es.count, (uint32_t)__popcll(wm));
+		sb = __shfl(sb, leader, 64);
+		sb += __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32),
+						__builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0));
+		if (want) {
+		const uint32_t s = sb;
 		if (s < es.cap) {
 			nsd_ext *e = es.ext + s;
 			uint32_t *z = (uint32_t *)e;   // entries past nlayers compare as zero
@@ -111,6 +125,7 @@ __device__ __forceinline__ void record_layer(WalkOut &w, int id, const ExtSink &
 		} else {
 			w.flags |= NSD_F_OVERFLOW;
 			w.slot = 0xFFFFFFFFu;
+		}
 		}
 	}
 	if (w.ext_on) {
@@ -238,13 +253,13 @@ __device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSin
 				if (x >= 0 && (uint64_t)x < l)
 					w.tail = d + (uint32_t)x;
 			}
-			next = lay3(proto);
+			next = s.lay3(proto);
 			break;
 		}
 		case NSD_OPS_IPV6:          // proto_ipv6.c:22-105
 		case NSD_OPS_IPV6_IN_IPV4:  // proto_ipv6_in_ipv4.c:20-24
 			if (len >= 40) {
-				next = lay3(s.b(start + 6));
+				next = s.lay3(s.b(start + 6));
 				w.data = start + 40;
 			}
 			break;
@@ -256,7 +271,7 @@ __device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSin
 			w.data = start + 2;
 			if (opt_len <= len - 2) {
 				w.data += opt_len;
-				next = lay3(s.b(start));
+				next = s.lay3(s.b(start));
 			}
 			break;
 		}
@@ -268,13 +283,13 @@ __device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSin
 			if (data_len <= len - 4) {
 				// type 0 pulls reserved + addresses, then the rest: same total
 				w.data += data_len;
-				next = lay3(s.b(start));
+				next = s.lay3(s.b(start));
 			}
 			break;
 		}
 		case NSD_OPS_IPV6_FRAGM:    // proto_ipv6_fragm.c:25-47
 			if (len >= 8) {
-				next = lay3(s.b(start));
+				next = s.lay3(s.b(start));
 				w.data = start + 8;
 			}
 			break;
@@ -286,7 +301,7 @@ __device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSin
 			if (hdr_len <= len - 12) {
 				if (hdr_len > 12)
 					w.data += hdr_len - 12;   // ICV bytes pulled one by one
-				next = lay3(s.b(start));
+				next = s.lay3(s.b(start));
 			}
 			break;
 		}
@@ -327,7 +342,7 @@ __device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSin
 					{ w.data = d; break; }
 			}
 			w.data = d + (uint32_t)mdl;
-			next = lay3(s.b(start));
+			next = s.lay3(s.b(start));
 			break;
 		}
 		case NSD_OPS_TCP:           // proto_tcp.c:63-107: leaf, options not pulled
@@ -381,6 +396,10 @@ __device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSin
 			w.flags |= NSD_F_HOST;
 			w.data = start;
 			break;
+		}
+		if constexpr (FAST) {
+			if (s.missed())   // a byte outside the staged window was needed
+				return true;
 		}
 		w.id = next;
 	}
