@@ -52,18 +52,24 @@ def wsum_for(cfg_key, n, lo):
     return None
 
 
-def cpu_baseline(cfg, n_sample, threads):
-    """CPU restatement (oracle, "port") timed on this host: fields-only walk
-    with `threads` threads over a bounded sample."""
-    frames, desc = T.make_batch(cfg, n_sample, lo=0)
+def cpu_baseline(cfg, n_sample, threads, seconds):
+    """CPU restatement (oracle, "port") timed on this host: the fields-only
+    walk (records + counters, no text) with `threads` threads, repeated over
+    one resident sample of `n_sample` packets until `seconds` have passed.
+    Returns (Mpkt/s, packets walked, seconds)."""
+    frames, desc = T.make_batch(cfg, n_sample, lo=0, threads=threads)
     lib = T.oracle()
     counters = np.zeros(64, dtype=np.uint64)
     rec = np.zeros(n_sample, dtype=T.REC_DTYPE)
-    t0 = time.perf_counter()
-    lib.nsor_dissect_batch_mt(frames.ctypes.data, desc.ctypes.data, n_sample, 1, T.PRINT_NORM,
-                              rec.ctypes.data, counters.ctypes.data, threads)
-    dt = time.perf_counter() - t0
-    return n_sample / dt / 1e6, dt
+    done, t0 = 0, time.perf_counter()
+    while True:
+        lib.nsor_dissect_batch_mt(frames.ctypes.data, desc.ctypes.data, n_sample, 1, T.PRINT_NORM,
+                                  rec.ctypes.data, counters.ctypes.data, threads)
+        done += n_sample
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return done / dt / 1e6, done, dt
 
 
 def main():
@@ -76,7 +82,8 @@ def main():
     ap.add_argument("--mode", type=int, default=nsd.PRINT_NORM)
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 21)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="packets in the CPU sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline duration")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,6 +147,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
+    # achievable streaming rate on this device: a 1 GiB
+    # device-to-device copy, read + write bytes / time
+    cbuf = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    cdst = torch.empty_like(cbuf)
+    for _ in range(2):
+        cdst.copy_(cbuf)
+    ce = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ce[0].record()
+    for _ in range(5):
+        cdst.copy_(cbuf)
+    ce[1].record()
+    torch.cuda.synchronize()
+    copy_gbs = 2 * cbuf.numel() * 5 / (ce[0].elapsed_time(ce[1]) * 1e-3) / 1e9
+    del cbuf, cdst
+
     cnt = counters.cpu().numpy().view(np.uint64)
     total_pkts = n * world
     assert int(cnt[nsd.CNT_PKTS]) == total_pkts, "counter check failed"
@@ -157,7 +179,9 @@ def main():
                     "traffic": None,
                     "read_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "bytes_per_pkt": {"read": round(read_b / n, 2), "write": REC_B},
-                    "kernel_ms": round(kern_ms, 4)}
+                    "kernel_ms": round(kern_ms, 4),
+                    "copy_gbs": round(copy_gbs, 1),
+                    "frac_of_copy": round(achieved / copy_gbs, 4)}
         prof = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
         if os.path.exists(prof):
             with open(prof) as f:
@@ -166,11 +190,13 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = min(os.cpu_count() or 1, 16)
-        v1, d1 = cpu_baseline(c["cfg"], args.cpu_sample // 4, 1)
-        vN, dN = cpu_baseline(c["cfg"], args.cpu_sample, threads)
+        v1, p1, d1 = cpu_baseline(c["cfg"], args.cpu_sample // 4, 1, args.cpu_seconds / 2)
+        vN, pN, dN = cpu_baseline(c["cfg"], args.cpu_sample, threads, args.cpu_seconds)
         cpu = {"value": round(vN, 3), "unit": "Mpkt/s", "cores": threads, "kind": "port",
-               "sample": f"{args.cpu_sample} packets of {args.config} (fields-only restatement walk,"
-                         f" {threads} threads, {dN:.1f} s); 1 thread: {v1:.3f} Mpkt/s"}
+               "sample": f"{args.config}: {pN} packets ({pN // args.cpu_sample} passes over a resident"
+                         f" {args.cpu_sample}-packet sample) in {dN:.1f} s, fields-only restatement"
+                         f" walk (oracle/nsd_oracle.c), {threads} threads; 1 thread:"
+                         f" {v1:.3f} Mpkt/s ({p1} packets, {d1:.1f} s)"}
 
     if rank == 0:
         out = {

@@ -13,9 +13,8 @@
 // load a global_load_dwordx4, whatever the frame's alignment; AF_PACKET rings
 // put the MAC header at 2 mod 16), and frame byte o sits at window position
 // o + m, m = off & 15.  Window bytes at frame offsets >= caplen are zeroed.
-// The window is stored transposed by dword: dword j of lane l's window lives
-// at win[j * 64 + l], so 64 lanes reading the same header offset hit 64
-// consecutive LDS dwords.
+// Each lane's window is one LDS row of 17 dwords (an odd stride): 64 lanes
+// reading the same header offset hit 64 different banks.
 //
 // Pass 1 (dissect_fast) finishes every packet whose chain resolves inside its
 // first 64 bytes, with the next tile's chunks and the tile after next's
@@ -34,6 +33,7 @@ constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
 constexpr int WIN = 64;          // bytes per staged window
 constexpr int CPP = WIN / 16;    // 16-byte chunks per window
+constexpr int ROW = WIN / 4 + 1; // window row stride in dwords (odd: conflict-free reads)
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
 {
@@ -54,7 +54,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
 // HBM (zero past caplen).
 template <bool FAST>
 struct LSrc {
-	const uint32_t *win;     // this wave's window array + lane
+	const uint32_t *win;     // this lane's window row
 	const uint8_t *lay3t;    // LDS copy of eth_lay3
 	const uint8_t *p;        // frame in HBM
 	uint32_t caplen;
@@ -62,7 +62,7 @@ struct LSrc {
 	uint32_t wb;             // aligned position of window byte 0 (multiple of 16)
 	mutable bool miss;
 
-	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return win[j * 64]; }
+	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return win[j]; }
 	__device__ __forceinline__ int lay3(uint32_t key) const { return lay3t[key & 255]; }
 	__device__ __forceinline__ bool missed() const { return miss; }
 	__device__ __forceinline__ uint8_t b(uint32_t o) const
@@ -161,61 +161,74 @@ struct Chunks {
 	uint4 v[CPP];
 };
 
+// Per-round view of packet q = (r * 64 + lane) / CPP: the raw descriptor and
+// the window base (bit 31 = not participating) are the only shuffled values.
+struct ChunkRef {
+	uint64_t off;
+	uint32_t cap, pos, lim;
+	bool part;
+};
+
+__device__ __forceinline__ ChunkRef chunk_ref(int r, int lane, uint64_t my_desc, uint32_t my_wbp)
+{
+	const int t = r * 64 + lane;
+	const int q = t / CPP, c = t % CPP;
+	const uint32_t dlo = __shfl((uint32_t)my_desc, q, 64);
+	const uint32_t dhi = __shfl((uint32_t)(my_desc >> 32), q, 64);
+	const uint32_t wbp = __shfl(my_wbp, q, 64);
+	ChunkRef k;
+	k.off = ((uint64_t)(dhi & 0xFF) << 32) | dlo;
+	k.cap = dhi >> 8;
+	k.part = !(wbp >> 31);
+	k.pos = (wbp & 0x7FFFFFFFu) + 16u * c;               // aligned position of the chunk
+	k.lim = k.cap + (dlo & 15);                          // first aligned position past the frame
+	return k;
+}
+
 // issue the loads (no wait): chunk c of lane q's window = aligned bytes
-// [A_q + wb_q + 16c, +16); skipped when the whole chunk is past caplen
-__device__ __forceinline__ void stage_load(Chunks &ch, const uint8_t *frames, uint64_t my_off,
-					   uint32_t my_cap, uint32_t my_wb, bool my_part, int lane)
+// [A_q + wb_q + 16c, +16); skipped when the whole chunk is past caplen.
+// my_wbp: window base (multiple of 16) | 0x80000000 when not participating.
+__device__ __forceinline__ void stage_load(Chunks &ch, const uint8_t *frames, uint64_t my_desc,
+					   uint32_t my_wbp, int lane)
 {
 #pragma unroll
 	for (int r = 0; r < CPP; r++) {
-		const int t = r * 64 + lane;
-		const int q = t / CPP, c = t % CPP;
-		const uint64_t off = __shfl(my_off, q, 64);
-		const uint32_t cap = __shfl(my_cap, q, 64);
-		const uint32_t wb = __shfl(my_wb, q, 64);
-		const bool part = __shfl((int)my_part, q, 64);
-		const uint32_t pos = wb + 16u * c;                 // aligned position of the chunk
-		const uint32_t m = (uint32_t)off & 15;
-		if (part && pos < cap + m)
-			ch.v[r] = *(const uint4 *)(frames + (off & ~15ull) + pos);
+		const ChunkRef k = chunk_ref(r, lane, my_desc, my_wbp);
+		if (k.part && k.pos < k.lim)
+			ch.v[r] = *(const uint4 *)(frames + (k.off & ~15ull) + k.pos);
 		else
 			ch.v[r] = make_uint4(0, 0, 0, 0);
 	}
 }
 
-// write the chunks to the transposed window, zeroing bytes at frame offsets
+// write the chunks to the window rows, zeroing bytes at frame offsets
 // >= caplen (aligned position >= caplen + m)
-__device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks &ch, uint64_t my_off,
-					    uint32_t my_cap, uint32_t my_wb, bool my_part, int lane)
+__device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks &ch, uint64_t my_desc,
+					    uint32_t my_wbp, int lane)
 {
 #pragma unroll
 	for (int r = 0; r < CPP; r++) {
+		const ChunkRef k = chunk_ref(r, lane, my_desc, my_wbp);
+		if (!k.part)
+			continue;
 		const int t = r * 64 + lane;
 		const int q = t / CPP, c = t % CPP;
-		const uint32_t m = (uint32_t)__shfl((uint32_t)my_off, q, 64) & 15;
-		const uint32_t cap = __shfl(my_cap, q, 64);
-		const uint32_t wb = __shfl(my_wb, q, 64);
-		const bool part = __shfl((int)my_part, q, 64);
-		if (!part)
-			continue;
-		const uint32_t pos = wb + 16u * c;
-		const uint32_t lim = cap + m;                      // first aligned position past the frame
 		uint32_t w[4] = { ch.v[r].x, ch.v[r].y, ch.v[r].z, ch.v[r].w };
-		if (pos + 16 > lim) {
+		if (k.pos + 16 > k.lim) {
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
-				const uint32_t bp = pos + 4 * j;
-				if (bp >= lim)
+				const uint32_t bp = k.pos + 4 * j;
+				if (bp >= k.lim)
 					w[j] = 0;
-				else if (bp + 4 > lim)
-					w[j] &= (1u << ((lim - bp) * 8)) - 1u;
+				else if (bp + 4 > k.lim)
+					w[j] &= (1u << ((k.lim - bp) * 8)) - 1u;
 			}
 		}
-		uint32_t *dst = wwin + (c * 4) * 64 + q;
+		uint32_t *dst = wwin + q * ROW + c * 4;   // a wave's writes are at most 2-way
 		dst[0] = w[0];
-		dst[64] = w[1];
-		dst[128] = w[2];
-		dst[192] = w[3];
+		dst[1] = w[1];
+		dst[2] = w[2];
+		dst[3] = w[3];
 	}
 }
 
@@ -226,39 +239,92 @@ __device__ __forceinline__ void wave_sync_lds()
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Per-lane ICMPv4 checksum over [a, a + nbytes) (nbytes even, csum.h:24-27):
-// 16-byte aligned loads; each byte is weighted by the parity of its distance
-// from `a` (1 for the low byte of an LE word, 256 for the high byte), which
-// makes the sum independent of the message's alignment.
-__device__ __forceinline__ uint16_t lane_csum(const uint8_t *frames, uint64_t a, uint32_t nbytes)
+// ICMPv4 checksum helpers (calc_csum over the whole message, csum.h:12-27).
+// Bytes are weighted by the parity of their distance from the message start
+// (1 for the low byte of an LE word, 256 for the high byte), which makes a
+// sum over 16-byte aligned loads independent of the message's alignment.
+// Partial sums may be folded early: folding keeps the value mod 0xFFFF and
+// keeps it non-zero, so the final fold gives the reference's result.
+__device__ __forceinline__ uint32_t csum_dword(uint32_t x, uint32_t lo, uint32_t s0, uint32_t endb,
+					       bool odd)
 {
-	const uint4 *p = (const uint4 *)(frames + (a & ~15ull));
-	const uint32_t s0 = (uint32_t)(a & 15), endb = s0 + nbytes;
-	const bool odd = a & 1;
-	uint32_t sum = 0;
-	auto add = [&](uint32_t x, uint32_t lo) {
-		if (lo + 4 <= s0 || lo >= endb)
-			return;
-		if (lo < s0)
-			x &= 0xFFFFFFFFu << (8 * (s0 - lo));
-		if (lo + 4 > endb)
-			x &= 0xFFFFFFFFu >> (8 * (lo + 4 - endb));
-		const uint32_t ev = x & 0x00FF00FFu, od = (x >> 8) & 0x00FF00FFu;
-		const uint32_t e2 = (ev & 0xFFFF) + (ev >> 16), o2 = (od & 0xFFFF) + (od >> 16);
-		sum += odd ? (e2 << 8) + o2 : e2 + (o2 << 8);
-	};
-	const uint32_t nchunk = (endb + 15) >> 4;
-#pragma unroll 4
-	for (uint32_t j = 0; j < nchunk; j++) {
-		const uint4 v = p[j];
-		add(v.x, 16 * j);
-		add(v.y, 16 * j + 4);
-		add(v.z, 16 * j + 8);
-		add(v.w, 16 * j + 12);
-	}
+	if (lo + 4 <= s0 || lo >= endb)
+		return 0;
+	if (lo < s0)
+		x &= 0xFFFFFFFFu << (8 * (s0 - lo));
+	if (lo + 4 > endb)
+		x &= 0xFFFFFFFFu >> (8 * (lo + 4 - endb));
+	const uint32_t ev = x & 0x00FF00FFu, od = (x >> 8) & 0x00FF00FFu;
+	const uint32_t e2 = (ev & 0xFFFF) + (ev >> 16), o2 = (od & 0xFFFF) + (od >> 16);
+	return odd ? (e2 << 8) + o2 : e2 + (o2 << 8);
+}
+
+__device__ __forceinline__ uint32_t csum_chunk(const uint4 &v, uint32_t lo, uint32_t s0, uint32_t endb,
+					       bool odd)
+{
+	return csum_dword(v.x, lo, s0, endb, odd) + csum_dword(v.y, lo + 4, s0, endb, odd) +
+	       csum_dword(v.z, lo + 8, s0, endb, odd) + csum_dword(v.w, lo + 12, s0, endb, odd);
+}
+
+__device__ __forceinline__ uint16_t csum_final(uint32_t sum)
+{
 	sum = (sum >> 16) + (sum & 0xffff);
 	sum += (sum >> 16);
 	return (uint16_t)~sum;
+}
+
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v)
+{
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		v += __shfl_xor(v, o, 64);
+	return v;
+}
+
+// Checksums of the messages the walks left pending (past the staged
+// window), wave-cooperatively: one message at a time per group slot, 64
+// lanes x 16 B = 1 KiB per coalesced load, four messages' loads in flight
+// together.  a = message start in `frames`, nbytes even (odd byte dropped).
+__device__ __forceinline__ void wave_icmp_csums(const uint8_t *frames, bool pend, uint64_t a,
+						 uint32_t nbytes, uint8_t &flags, int lane)
+{
+	constexpr int G = 4;
+	uint64_t pm = __ballot(pend);
+	while (pm) {
+		int L[G];
+		uint32_t s0[G], endb[G], nch[G];
+		const uint4 *p[G];
+		uint4 v[G];
+#pragma unroll
+		for (int t = 0; t < G; t++) {
+			L[t] = pm ? __ffsll((unsigned long long)pm) - 1 : -1;
+			pm &= pm - 1;
+			nch[t] = 0;
+			if (L[t] >= 0) {
+				const uint32_t alo = __builtin_amdgcn_readlane((uint32_t)a, L[t]);
+				const uint32_t ahi = __builtin_amdgcn_readlane((uint32_t)(a >> 32), L[t]);
+				const uint32_t nb = __builtin_amdgcn_readlane(nbytes, L[t]);
+				s0[t] = alo & 15;
+				endb[t] = s0[t] + nb;
+				nch[t] = (endb[t] + 15) >> 4;
+				p[t] = (const uint4 *)(frames + ((((uint64_t)ahi << 32) | alo) & ~15ull));
+			}
+			v[t] = (uint32_t)lane < nch[t] ? p[t][lane] : make_uint4(0, 0, 0, 0);
+		}
+#pragma unroll
+		for (int t = 0; t < G; t++) {
+			if (L[t] < 0)
+				break;
+			const bool odd = s0[t] & 1;
+			uint32_t sum = csum_chunk(v[t], 16 * lane, s0[t], endb[t], odd);
+			for (uint32_t j = lane + 64; j < nch[t]; j += 64)
+				sum += csum_chunk(p[t][j], 16 * j, s0[t], endb[t], odd);
+			sum = (sum >> 16) + (sum & 0xffff);
+			sum = wave_sum32(sum);
+			if (lane == L[t] && csum_final(sum))
+				flags |= NSD_F_ICMP_BAD;
+		}
+	}
 }
 
 // record words of a finished walk (layout of nsd_rec)
@@ -282,31 +348,35 @@ __device__ __forceinline__ uint4 pack_record(const WalkOut &w)
 	return r;
 }
 
+// Per-wave flag counters: wave-uniform (ballot + popcount, scalar registers);
+// only the byte count is per lane.
 struct FlagCnt {
 	uint32_t pkts = 0, ipbad = 0, icmpbad = 0, host = 0, ext = 0, ovf = 0, trim = 0;
 	uint64_t bytes = 0;
-	__device__ __forceinline__ void add(const WalkOut &w, uint32_t caplen)
+	__device__ __forceinline__ static uint32_t pc(bool c) { return (uint32_t)__popcll(__ballot(c)); }
+	__device__ __forceinline__ void add(const WalkOut &w, uint32_t caplen, bool on)
 	{
-		pkts++;
-		bytes += caplen;
-		ipbad += w.ip_csum != 0;
-		icmpbad += (w.flags & NSD_F_ICMP_BAD) != 0;
-		host += (w.flags & NSD_F_HOST) != 0;
-		ext += w.need_ext;
-		ovf += (w.flags & NSD_F_OVERFLOW) != 0;
-		trim += w.tail < caplen;
+		pkts += pc(on);
+		ipbad += pc(on && w.ip_csum != 0);
+		icmpbad += pc(on && (w.flags & NSD_F_ICMP_BAD));
+		host += pc(on && (w.flags & NSD_F_HOST));
+		ext += pc(on && w.need_ext);
+		ovf += pc(on && (w.flags & NSD_F_OVERFLOW));
+		trim += pc(on && w.tail < caplen);
+		if (on)
+			bytes += caplen;
 	}
-	// wave reduce -> block LDS counters
+	// -> block LDS counters
 	__device__ __forceinline__ void flush(unsigned long long *s_cnt, int lane) const
 	{
 		const uint32_t vals[7] = { pkts, ipbad, icmpbad, host, ext, ovf, trim };
 		const int idx[7] = { NSD_CNT_PKTS, NSD_CNT_IP_BAD, NSD_CNT_ICMP_BAD, NSD_CNT_HOST,
 				     NSD_CNT_EXT, NSD_CNT_OVERFLOW, NSD_CNT_TRIM };
+		if (lane == 0) {
 #pragma unroll
-		for (int k = 0; k < 7; k++) {
-			const uint64_t v = wave_sum64(vals[k]);
-			if (lane == 0 && v)
-				atomicAdd(&s_cnt[idx[k]], (unsigned long long)v);
+			for (int k = 0; k < 7; k++)
+				if (vals[k])
+					atomicAdd(&s_cnt[idx[k]], (unsigned long long)vals[k]);
 		}
 		const uint64_t b = wave_sum64(bytes);
 		if (lane == 0 && b)
@@ -336,9 +406,10 @@ template <int MODE>
 __global__ __launch_bounds__(BLOCK) void dissect_fast(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n,
 	int start_id, uint4 *__restrict__ rec, unsigned long long *__restrict__ counters,
-	uint32_t *__restrict__ queue, uint32_t region, uint32_t *__restrict__ qblk)
+	uint32_t *__restrict__ queue, uint32_t region, uint32_t *__restrict__ qblk,
+	uint64_t *__restrict__ pend)
 {
-	__shared__ uint32_t s_win[WAVES][(WIN / 4) * 64];
+	__shared__ uint32_t s_win[WAVES][64 * ROW];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
 	__shared__ uint8_t s_lay3[256];
 	__shared__ uint32_t s_qn;
@@ -351,6 +422,9 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 
 	const uint32_t stride = gridDim.x * BLOCK;
 	uint32_t *const bq = queue + (size_t)blockIdx.x * region;   // this block's queue region
+	// this wave's pending-checksum list (a wave visits region / WAVES packets)
+	uint64_t *const wq = pend + ((size_t)blockIdx.x * WAVES + wv) * (region / WAVES);
+	uint32_t npend = 0;
 	FlagCnt fc;
 	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
 
@@ -358,10 +432,10 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		// every process() is NULL: no chain (dissector.c:51-53)
 		for (; base < n; base += stride) {
 			const uint32_t i = base + lane;
+			fc.pkts += FlagCnt::pc(i < n);
 			if (i < n) {
 				const uint32_t caplen = NSD_DESC_CAPLEN(desc[i]);
 				rec[i] = make_uint4(0, caplen << 16, 0, 0);
-				fc.pkts++;
 				fc.bytes += caplen;
 			}
 		}
@@ -377,7 +451,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
 	uint64_t d1 = (base + stride + lane < n) ? desc[base + stride + lane] : 0;
 	Chunks ch;
-	stage_load(ch, frames, NSD_DESC_OFF(d0), NSD_DESC_CAPLEN(d0), 0, base + lane < n, lane);
+	stage_load(ch, frames, d0, base + lane < n ? 0u : 0x80000000u, lane);
 
 	for (; base < n; base += stride) {
 		const uint32_t i = base + lane;
@@ -385,24 +459,38 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		const uint64_t off = NSD_DESC_OFF(d0);
 		const uint32_t caplen = NSD_DESC_CAPLEN(d0);
 
-		stage_write(&s_win[wv][0], ch, off, caplen, 0, valid, lane);
+		stage_write(&s_win[wv][0], ch, d0, valid ? 0u : 0x80000000u, lane);
 		// prefetch: descriptors of tile t+2, chunks of tile t+1
 		const uint32_t b2 = base + 2 * stride;
 		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
 		const uint32_t b1 = base + stride;
 		if (b1 < n)
-			stage_load(ch, frames, NSD_DESC_OFF(d1), NSD_DESC_CAPLEN(d1), 0, b1 + lane < n, lane);
+			stage_load(ch, frames, d1, b1 + lane < n ? 0u : 0x80000000u, lane);
 		wave_sync_lds();
 
 		WalkOut w;
 		walk_init(w, caplen, valid ? start_id : 0);
 		bool deferred = false;
 		if (valid) {
-			const LSrc<true> src{ &s_win[wv][lane], s_lay3, frames + off, caplen,
+			const LSrc<true> src{ &s_win[wv][lane * ROW], s_lay3, frames + off, caplen,
 					      (uint32_t)off & 15, 0, false };
-			deferred = walk<MODE, true>(src, caplen, ExtSink{ nullptr, 0, nullptr }, w, 0);
+#ifdef NSD_X_NOWALK
+			w.chain = src.dw(3) & 0x3FF; w.n = 2; w.data = 42;
+#else
+			deferred = fast_walk<MODE>(src, caplen, w);
+#endif
 		}
 		wave_sync_lds();
+		if (MODE == PRINT_NORM) {
+			// ICMPv4 messages past the window: checksummed by the wave after
+			// the tile loop (their records are patched if the sum is bad)
+			const bool pnd = w.icmp_pend && !deferred;
+			const uint64_t pmask = __ballot(pnd);
+			if (pnd)
+				wq[npend + lanes_below(pmask)] = (uint64_t)i |
+					(uint64_t)(w.icmp_off | (w.icmp_len & 0xFFFF) << 8 | (w.n | w.flags) << 24) << 32;
+			npend += (uint32_t)__popcll(pmask);
+		}
 
 		const uint64_t dm = __ballot(deferred);
 		if (dm) {
@@ -436,12 +524,24 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 					key = 0xFFFFFFFFu;
 			}
 		}
-		if (done) {
+		if (done)
 			rec[i] = pack_record(w);
-			fc.add(w, caplen);
-		}
+		fc.add(w, caplen, done);
 		d0 = d1;
 		d1 = d2;
+	}
+	// drain this wave's pending checksums (entries and records were written
+	// by this wave: its memory operations complete in order)
+	for (uint32_t k0 = 0; k0 < npend; k0 += 64) {
+		const bool on = k0 + lane < npend;
+		const uint64_t e = on ? wq[k0 + lane] : 0;
+		const uint32_t i = (uint32_t)e, meta = (uint32_t)(e >> 32);
+		const uint64_t off = on ? NSD_DESC_OFF(desc[i]) : 0;
+		uint8_t fl = 0;
+		wave_icmp_csums(frames, on, off + (meta & 0xFF), (meta >> 8) & 0xFFFEu, fl, lane);
+		if (fl)
+			((uint8_t *)rec)[(size_t)i * 16 + 10] = (uint8_t)(meta >> 24) | NSD_F_ICMP_BAD;
+		fc.icmpbad += FlagCnt::pc(fl != 0);
 	}
 	fc.flush(s_cnt, lane);
 	block_flush(s_cnt, counters);
@@ -457,7 +557,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	uint32_t *__restrict__ ext_count, unsigned long long *__restrict__ counters,
 	const uint32_t *__restrict__ queue, uint32_t region, const uint32_t *__restrict__ qblk)
 {
-	__shared__ uint32_t s_win[WAVES][(WIN / 4) * 64];
+	__shared__ uint32_t s_win[WAVES][64 * ROW];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
 	__shared__ uint8_t s_lay3[256];
 
@@ -489,12 +589,13 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 		// restages those windows at the lanes' cursors and resumes them
 		for (;;) {
 			Chunks ch;
-			stage_load(ch, frames, off, caplen, wb, part, lane);
-			stage_write(&s_win[wv][0], ch, off, caplen, wb, part, lane);
+			const uint32_t wbp = wb | (part ? 0u : 0x80000000u);
+			stage_load(ch, frames, d, wbp, lane);
+			stage_write(&s_win[wv][0], ch, d, wbp, lane);
 			wave_sync_lds();
 			bool susp = false;
 			if (part) {
-				const LSrc<false> src{ &s_win[wv][lane], s_lay3, frames + off, caplen, m, wb, false };
+				const LSrc<false> src{ &s_win[wv][lane * ROW], s_lay3, frames + off, caplen, m, wb, false };
 				susp = walk<MODE, false>(src, caplen, es, w, wc);
 			}
 			wave_sync_lds();
@@ -504,10 +605,8 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 			if (susp)
 				wb = (w.data + m) & ~15u;
 		}
-		if (MODE == PRINT_NORM && w.icmp_pend) {
-			if (lane_csum(frames, off + w.icmp_off, w.icmp_len & ~1u))
-				w.flags |= NSD_F_ICMP_BAD;
-		}
+		if (MODE == PRINT_NORM)
+			wave_icmp_csums(frames, w.icmp_pend, off + w.icmp_off, w.icmp_len & ~1u, w.flags, lane);
 		if (!valid)
 			continue;
 		if (w.ext_on) {
@@ -516,7 +615,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 			e->nlayers = (uint16_t)(w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS);
 		}
 		rec[i] = pack_record(w);
-		fc.add(w, caplen);
+		fc.add(w, caplen, true);
 	}
 	fc.flush(s_cnt, lane);
 	block_flush(s_cnt, counters);
@@ -537,10 +636,16 @@ static uint32_t region_for(uint32_t n, uint32_t blocks)
 	return (uint32_t)(((n + stride - 1) / stride) * nsd::BLOCK);
 }
 
+// worst case over grids: sum of regions <= n + blocks * BLOCK
+static size_t region_slots(uint32_t n)
+{
+	return ((size_t)n + (size_t)NSD_MAX_GRID * nsd::BLOCK + 1) & ~(size_t)1;
+}
+
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
-	// worst case over grids: sum of regions <= n + blocks * BLOCK
-	return 4 * (size_t)NSD_MAX_GRID + 4 * ((size_t)n + (size_t)NSD_MAX_GRID * nsd::BLOCK);
+	// qblk, the deferral queue (u32 per slot), the pending-checksum lists (u64 per slot)
+	return 4 * (size_t)NSD_MAX_GRID + 4 * region_slots(n) + 8 * region_slots(n);
 }
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
@@ -560,9 +665,21 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	}
 	const uint32_t waves = (n + 63) / 64;
 	uint32_t blocks = (waves + WAVES - 1) / WAVES;
-	// persistent grid: enough resident blocks to fill every CU, the rest
-	// grid-strides (counters then cost one flush per block)
-	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)s_cus * 8;
+	// persistent grid: exactly the blocks that are resident together (CUs x
+	// the pass-1 kernel's occupancy), so no block waits for a second round;
+	// every block grid-strides (counters then cost one flush per block)
+	static int s_occ[3] = { 0, 0, 0 };
+	const int mi = mode == PRINT_NORM ? 0 : mode == PRINT_LESS ? 1 : 2;
+	if (!s_occ[mi]) {
+		const void *f = mi == 0 ? (const void *)dissect_fast<PRINT_NORM>
+			      : mi == 1 ? (const void *)dissect_fast<PRINT_LESS>
+					: (const void *)dissect_fast<PRINT_HEX>;
+		int occ = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, BLOCK, 0) != hipSuccess || occ < 1)
+			occ = 4;
+		s_occ[mi] = occ;
+	}
+	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)(s_cus * s_occ[mi]);
 	if (cap_blocks > NSD_MAX_GRID)
 		cap_blocks = NSD_MAX_GRID;
 	if (blocks > cap_blocks)
@@ -572,24 +689,25 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	uint4 *rec = (uint4 *)d_rec;
 	uint32_t *qblk = (uint32_t *)d_ws;
 	uint32_t *queue = qblk + NSD_MAX_GRID;
+	uint64_t *pend = (uint64_t *)(queue + region_slots(n));
 	switch (mode) {
 	case PRINT_NORM:
 		hipLaunchKernelGGL(dissect_fast<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk);
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend);
 		hipLaunchKernelGGL(dissect_general<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
 				   region, qblk);
 		break;
 	case PRINT_LESS:
 		hipLaunchKernelGGL(dissect_fast<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk);
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend);
 		hipLaunchKernelGGL(dissect_general<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
 				   region, qblk);
 		break;
 	default:
 		hipLaunchKernelGGL(dissect_fast<PRINT_HEX>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk);
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend);
 		break;
 	}
 	return hipGetLastError() == hipSuccess ? 0 : -2;

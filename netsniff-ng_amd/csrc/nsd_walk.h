@@ -129,7 +129,11 @@ __device__ __forceinline__ void record_layer(WalkOut &w, int id, const ExtSink &
 		}
 	}
 	if (w.ext_on) {
+#ifdef NSD_X_NOEXTW
+		if (0) {
+#else
 		if (k < NSD_EXT_MAX_LAYERS) {
+#endif
 			es.ext[w.slot].id[k] = (uint8_t)id;
 			es.ext[w.slot].off[k] = (uint16_t)w.data;
 		} else {
@@ -404,6 +408,152 @@ __device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSin
 		w.id = next;
 	}
 	return false;
+}
+
+// Straight-line walk for the common chains (pass 1): Ethernet, up to two
+// 802.1Q / 802.1ad tags, IPv4 or IPv6, then TCP / UDP / ICMPv4 / ICMPv6 /
+// ESP / NoNext (or a host-rendered leaf: ARP, LLDP, IGMP, DCCP).  Same
+// semantics as walk() for every packet it finishes (the per-layer comments
+// there cite the reference); anything else (MPLS, deeper tag stacks,
+// extension headers, IPv6-in-IPv4, bytes past the staged window) returns true
+// and the packet goes to pass 2.  No loop, no per-layer dispatch switch.
+template <int MODE, class Src>
+__device__ __forceinline__ bool fast_walk(const Src &s, uint32_t caplen, WalkOut &w)
+{
+	uint32_t n = 0;
+	auto rec = [&](int id, uint32_t at) {
+		w.chain |= (uint32_t)id << (5 * n);
+		if (n < 4)
+			w.offA |= (uint64_t)at << (16 * n);
+		else
+			w.offB |= at << (16 * (n - 4));
+		n++;
+	};
+	if (w.id != NSD_OPS_ETHERNET)
+		return true;   // other link types: pass 2
+	rec(NSD_OPS_ETHERNET, 0);
+	if (caplen < 14) {
+		w.n = n;
+		return false;
+	}
+	uint32_t d = 14;
+	int next = lay2(s.be16(12));
+#pragma unroll
+	for (int t = 0; t < 2; t++) {
+		if (next != NSD_OPS_VLAN && next != NSD_OPS_QINQ)
+			break;
+		rec(next, d);
+		if (caplen - d < 4) {
+			w.data = d;
+			w.n = n;
+			return s.missed();
+		}
+		next = lay2(s.be16(d + 2));
+		d += 4;
+	}
+	w.data = d;
+	uint32_t d2;
+	int l4;
+	if (next == NSD_OPS_IPV4) {
+		rec(NSD_OPS_IPV4, d);
+		if (caplen - d < 20) {
+			w.n = n;
+			return s.missed();
+		}
+		const uint32_t ihl = s.b(d) & 0xF;
+		const uint32_t proto = s.b(d + 9);
+		if (MODE == PRINT_NORM) {
+			if (!s.in_window(d, ihl * 4u))
+				return true;
+			w.ip_csum = calc_csum(s, d, ihl * 2u);
+		}
+		d2 = d + 20;
+		uint32_t l = caplen - d2;
+		const uint32_t opts = (ihl > 5 ? ihl : 5) * 4u - 20u;
+		if (opts <= l) { d2 += opts; l -= opts; }
+		if (MODE == PRINT_NORM) {
+			const int32_t x = (int32_t)s.be16(d + 2) - (int32_t)(ihl * 4);
+			if (x >= 0 && (uint32_t)x < l)
+				w.tail = d2 + (uint32_t)x;
+		}
+		l4 = s.lay3(proto);
+	} else if (next == NSD_OPS_IPV6) {
+		rec(NSD_OPS_IPV6, d);
+		if (caplen - d < 40) {
+			w.n = n;
+			return s.missed();
+		}
+		d2 = d + 40;
+		l4 = s.lay3(s.b(d + 6));
+	} else if (next == NSD_OPS_ARP || next == NSD_OPS_LLDP) {
+		rec(next, d);
+		w.flags |= NSD_F_HOST;
+		w.n = n;
+		return s.missed();
+	} else if (next == 0) {
+		w.n = n;
+		return s.missed();
+	} else {
+		return true;   // MPLS, a third tag
+	}
+	w.data = d2;
+	const uint32_t len = w.tail - d2;
+	switch (l4) {
+	case 0:
+		break;
+	case NSD_OPS_TCP:
+		rec(l4, d2);
+		if (len >= 20) w.data = d2 + 20;
+		break;
+	case NSD_OPS_UDP:
+	case NSD_OPS_IP_ESP:
+		rec(l4, d2);
+		if (len >= 8) w.data = d2 + 8;
+		break;
+	case NSD_OPS_IPV6_NO_NEXT:
+		rec(l4, d2);
+		break;
+	case NSD_OPS_ICMPV4:
+		rec(l4, d2);
+		if (len >= 8) {
+			w.data = d2 + 8;
+			if (MODE == PRINT_NORM) {
+				if (!s.in_window(d2, len & ~1u)) {
+					// message past the window: the wave sums it after the walk
+					w.icmp_pend = true;
+					w.icmp_off = d2;
+					w.icmp_len = len;
+				} else if (calc_csum(s, d2, len >> 1)) {
+					w.flags |= NSD_F_ICMP_BAD;
+				}
+			}
+		}
+		break;
+	case NSD_OPS_ICMPV6:
+		rec(l4, d2);
+		if (len >= 4) {
+			w.data = d2 + 4;
+			if (MODE == PRINT_NORM) {
+				const uint8_t type = s.b(d2);
+				if (type >= 130 && type <= 154) {
+					w.flags |= NSD_F_HOST;
+					w.data = d2;
+				} else if (((type >= 1 && type <= 4) || type == 128 || type == 129) && len - 4 >= 4) {
+					w.data = d2 + 8;
+				}
+			}
+		}
+		break;
+	case NSD_OPS_IGMP:
+	case NSD_OPS_DCCP:
+		rec(l4, d2);
+		w.flags |= NSD_F_HOST;
+		break;
+	default:
+		return true;   // extension headers, AH, IPv6-in-IPv4
+	}
+	w.n = n;
+	return s.missed();
 }
 
 } // namespace nsd

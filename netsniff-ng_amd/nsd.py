@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnsdissect.so")
+LIB_PATH = os.environ.get("NSD_LIB") or os.path.join(HERE, "libnsdissect.so")
 
 PRINT_NORM, PRINT_LESS, PRINT_HEX, PRINT_ASCII, PRINT_HEX_ASCII, PRINT_NONE = range(6)
 LINKTYPE_EN10MB = 1
