@@ -159,69 +159,60 @@ struct WaveCnt {
 
 struct Chunks {
 	uint4 v[CPP];
+	uint32_t nv;   // valid bytes of chunk r (0..16) in bits 8r..8r+7
 };
 
-// Per-round view of packet q = (r * 64 + lane) / CPP: the raw descriptor and
-// the window base (bit 31 = not participating) are the only shuffled values.
-struct ChunkRef {
-	uint64_t off;
-	uint32_t cap, pos, lim;
-	bool part;
-};
-
-__device__ __forceinline__ ChunkRef chunk_ref(int r, int lane, uint64_t my_desc, uint32_t my_wbp)
-{
-	const int t = r * 64 + lane;
-	const int q = t / CPP, c = t % CPP;
-	const uint32_t dlo = __shfl((uint32_t)my_desc, q, 64);
-	const uint32_t dhi = __shfl((uint32_t)(my_desc >> 32), q, 64);
-	const uint32_t wbp = __shfl(my_wbp, q, 64);
-	ChunkRef k;
-	k.off = ((uint64_t)(dhi & 0xFF) << 32) | dlo;
-	k.cap = dhi >> 8;
-	k.part = !(wbp >> 31);
-	k.pos = (wbp & 0x7FFFFFFFu) + 16u * c;               // aligned position of the chunk
-	k.lim = k.cap + (dlo & 15);                          // first aligned position past the frame
-	return k;
-}
-
-// issue the loads (no wait): chunk c of lane q's window = aligned bytes
-// [A_q + wb_q + 16c, +16); skipped when the whole chunk is past caplen.
-// my_wbp: window base (multiple of 16) | 0x80000000 when not participating.
+// issue the loads (no wait): in round r, lane (q * CPP + c) % 64 loads chunk
+// c of packet q's window = aligned bytes [A_q + wb_q + 16c, +16), skipped when
+// the chunk lies wholly past caplen (or the packet does not participate).
+// Only the descriptor (and, with WB, the window base) is shuffled; the count
+// of valid bytes per chunk is kept for stage_write, which then needs no
+// shuffles.  my_wbp: window base (multiple of 16) | 0x80000000 when not
+// participating; without WB every packet with caplen > 0 participates at 0.
+template <bool WB>
 __device__ __forceinline__ void stage_load(Chunks &ch, const uint8_t *frames, uint64_t my_desc,
 					   uint32_t my_wbp, int lane)
 {
+	ch.nv = 0;
 #pragma unroll
 	for (int r = 0; r < CPP; r++) {
-		const ChunkRef k = chunk_ref(r, lane, my_desc, my_wbp);
-		if (k.part && k.pos < k.lim)
-			ch.v[r] = *(const uint4 *)(frames + (k.off & ~15ull) + k.pos);
-		else
-			ch.v[r] = make_uint4(0, 0, 0, 0);
+		const int t = r * 64 + lane;
+		const int q = t / CPP, c = t % CPP;
+		const uint32_t dlo = __shfl((uint32_t)my_desc, q, 64);
+		const uint32_t dhi = __shfl((uint32_t)(my_desc >> 32), q, 64);
+		uint32_t pos = 16u * c;
+		bool part = true;
+		if constexpr (WB) {
+			const uint32_t wbp = __shfl(my_wbp, q, 64);
+			part = !(wbp >> 31);
+			pos += wbp & 0x7FFFFFFFu;
+		}
+		const uint32_t lim = (dhi >> 8) + (dlo & 15);   // first aligned position past the frame
+		const uint32_t nv = part && pos < lim ? min(lim - pos, 16u) : 0u;
+		const uint64_t off = ((uint64_t)(dhi & 0xFF) << 32) | dlo;
+		ch.v[r] = nv ? *(const uint4 *)(frames + (off & ~15ull) + pos) : make_uint4(0, 0, 0, 0);
+		ch.nv |= nv << (8 * r);
 	}
 }
 
-// write the chunks to the window rows, zeroing bytes at frame offsets
-// >= caplen (aligned position >= caplen + m)
-__device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks &ch, uint64_t my_desc,
-					    uint32_t my_wbp, int lane)
+// write the chunks to the window rows (row q, dwords 4c..4c+3), zeroing the
+// bytes at frame offsets >= caplen
+__device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks &ch, int lane)
 {
 #pragma unroll
 	for (int r = 0; r < CPP; r++) {
-		const ChunkRef k = chunk_ref(r, lane, my_desc, my_wbp);
-		if (!k.part)
-			continue;
 		const int t = r * 64 + lane;
 		const int q = t / CPP, c = t % CPP;
+		const uint32_t nv = (ch.nv >> (8 * r)) & 0xFF;
 		uint32_t w[4] = { ch.v[r].x, ch.v[r].y, ch.v[r].z, ch.v[r].w };
-		if (k.pos + 16 > k.lim) {
+		if (nv < 16) {
 #pragma unroll
 			for (int j = 0; j < 4; j++) {
-				const uint32_t bp = k.pos + 4 * j;
-				if (bp >= k.lim)
+				const uint32_t bp = 4 * j;
+				if (bp >= nv)
 					w[j] = 0;
-				else if (bp + 4 > k.lim)
-					w[j] &= (1u << ((k.lim - bp) * 8)) - 1u;
+				else if (bp + 4 > nv)
+					w[j] &= (1u << ((nv - bp) * 8)) - 1u;
 			}
 		}
 		uint32_t *dst = wwin + q * ROW + c * 4;   // a wave's writes are at most 2-way
@@ -451,7 +442,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
 	uint64_t d1 = (base + stride + lane < n) ? desc[base + stride + lane] : 0;
 	Chunks ch;
-	stage_load(ch, frames, d0, base + lane < n ? 0u : 0x80000000u, lane);
+	stage_load<false>(ch, frames, d0, 0, lane);
 
 	for (; base < n; base += stride) {
 		const uint32_t i = base + lane;
@@ -459,13 +450,13 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		const uint64_t off = NSD_DESC_OFF(d0);
 		const uint32_t caplen = NSD_DESC_CAPLEN(d0);
 
-		stage_write(&s_win[wv][0], ch, d0, valid ? 0u : 0x80000000u, lane);
+		stage_write(&s_win[wv][0], ch, lane);
 		// prefetch: descriptors of tile t+2, chunks of tile t+1
 		const uint32_t b2 = base + 2 * stride;
 		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
 		const uint32_t b1 = base + stride;
 		if (b1 < n)
-			stage_load(ch, frames, d1, b1 + lane < n ? 0u : 0x80000000u, lane);
+			stage_load<false>(ch, frames, d1, 0, lane);
 		wave_sync_lds();
 
 		WalkOut w;
@@ -590,8 +581,8 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 		for (;;) {
 			Chunks ch;
 			const uint32_t wbp = wb | (part ? 0u : 0x80000000u);
-			stage_load(ch, frames, d, wbp, lane);
-			stage_write(&s_win[wv][0], ch, d, wbp, lane);
+			stage_load<true>(ch, frames, d, wbp, lane);
+			stage_write(&s_win[wv][0], ch, lane);
 			wave_sync_lds();
 			bool susp = false;
 			if (part) {
