@@ -225,6 +225,42 @@ void nsd_lookup_cleanup(void);
 long nsd_tprintf_wrap(const char *in, size_t len, int cols, long *state,
 		      char *out, size_t cap);
 
+/* Pipelined host-batch path (the RX loop's batches, SURVEY 8f.2: e.g. one
+ * TPACKET_V3 block per batch, walk_t3_block netsniff-ng.c:991-1039).  Each
+ * submitted batch is copied to the device, walked and its records copied
+ * back on its own stream slot; up to `depth` batches are in flight, so the
+ * copies of one batch overlap the walk of another.  The caller's buffers
+ * belong to the pipe from submit until the batch completes (nsd_pipe_wait);
+ * pinned buffers (nsd_host_alloc / nsd_host_register) make the copies
+ * asynchronous, pageable ones still work but serialise them.
+ * Batches complete in submission order.
+ *
+ * nsd_pipe_create: capacities per batch (packets, frame bytes, ext slots),
+ * 1 <= depth <= 8.  NULL on failure (no GPU, no memory, bad arguments).
+ * nsd_pipe_submit: validates like dissector_entry_batch, then enqueues; when
+ * all slots are busy it first completes the oldest batch (its status is
+ * returned through that batch's *status, see below).  rec[n] receives the
+ * records, ext[ext_cap] / *ext_count the spilled layers, counters[64] (may
+ * be NULL) this batch's counters, *status (may be NULL) the batch's final
+ * status.  Returns NSD_OK if enqueued, else NSD_ERR_*.
+ * nsd_pipe_wait: completes the oldest in-flight batch, returns its status,
+ * or 1 when nothing is in flight.  nsd_pipe_drain: completes all. */
+typedef struct nsd_pipe nsd_pipe;
+nsd_pipe *nsd_pipe_create(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_cap,
+			  int depth, int linktype, int mode);
+int nsd_pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
+		    const nsd_desc_t *desc, uint32_t n, nsd_rec *rec, nsd_ext *ext,
+		    uint32_t *ext_count, uint64_t *counters, int *status);
+int nsd_pipe_wait(nsd_pipe *p);
+int nsd_pipe_drain(nsd_pipe *p);
+void nsd_pipe_destroy(nsd_pipe *p);
+
+/* Pinned host memory for the pipe's buffers. */
+void *nsd_host_alloc(size_t len);
+void nsd_host_free(void *ptr);
+int nsd_host_register(void *ptr, size_t len);
+int nsd_host_unregister(void *ptr);
+
 /* Library / device info. */
 const char *nsd_version(void);
 int nsd_device_count(void);

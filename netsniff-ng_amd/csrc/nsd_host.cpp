@@ -136,7 +136,10 @@ bool grow(T *&p, size_t &cap, size_t need)
 	return true;
 }
 
-int start_for(int linktype)
+} // namespace
+
+// linktype -> first ops (dissector.c:75-103); shared with nsd_pipe.cpp
+__attribute__((visibility("hidden"))) int nsd_start_for(int linktype)
 {
 	auto is = [&](uint32_t v) { return (uint32_t)linktype == v || (uint32_t)linktype == __builtin_bswap32(v); };
 	if (is(NSD_LINKTYPE_EN10MB)) return NSD_OPS_ETHERNET;
@@ -145,6 +148,9 @@ int start_for(int linktype)
 	if (is(NSD_LINKTYPE_NETLINK)) return NSD_OPS_NLMSG;
 	return 0;   // unknown link type: start at none_ops (dissector.c:100-103)
 }
+
+namespace {
+int start_for(int linktype) { return nsd_start_for(linktype); }
 } // namespace
 
 // ---- batch extension ---------------------------------------------------

@@ -34,6 +34,9 @@ constexpr int WAVES = BLOCK / 64;
 constexpr int WIN = 64;          // bytes per staged window
 constexpr int CPP = WIN / 16;    // 16-byte chunks per window
 constexpr int ROW = WIN / 4 + 1; // window row stride in dwords (odd: conflict-free reads)
+#ifndef NSD_DRAIN_G
+#define NSD_DRAIN_G 8              // pending checksums with loads in flight together per wave
+#endif
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
 {
@@ -157,9 +160,10 @@ struct WaveCnt {
 // loads chunk c of packet q's window, so the CPP chunks of one packet are
 // read by consecutive lanes as one contiguous, 16-byte aligned segment.
 
+static_assert(CPP * 6 <= 32, "chunk valid counts must fit one word");
 struct Chunks {
 	uint4 v[CPP];
-	uint32_t nv;   // valid bytes of chunk r (0..16) in bits 8r..8r+7
+	uint32_t nv;   // valid bytes of chunk r (0..16) in bits 6r..6r+5
 };
 
 // issue the loads (no wait): in round r, lane (q * CPP + c) % 64 loads chunk
@@ -191,7 +195,7 @@ __device__ __forceinline__ void stage_load(Chunks &ch, const uint8_t *frames, ui
 		const uint32_t nv = part && pos < lim ? min(lim - pos, 16u) : 0u;
 		const uint64_t off = ((uint64_t)(dhi & 0xFF) << 32) | dlo;
 		ch.v[r] = nv ? *(const uint4 *)(frames + (off & ~15ull) + pos) : make_uint4(0, 0, 0, 0);
-		ch.nv |= nv << (8 * r);
+		ch.nv |= nv << (6 * r);
 	}
 }
 
@@ -203,7 +207,7 @@ __device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks &ch, in
 	for (int r = 0; r < CPP; r++) {
 		const int t = r * 64 + lane;
 		const int q = t / CPP, c = t % CPP;
-		const uint32_t nv = (ch.nv >> (8 * r)) & 0xFF;
+		const uint32_t nv = (ch.nv >> (6 * r)) & 0x3F;
 		uint32_t w[4] = { ch.v[r].x, ch.v[r].y, ch.v[r].z, ch.v[r].w };
 		if (nv < 16) {
 #pragma unroll
@@ -231,30 +235,52 @@ __device__ __forceinline__ void wave_sync_lds()
 }
 
 // ICMPv4 checksum helpers (calc_csum over the whole message, csum.h:12-27).
-// Bytes are weighted by the parity of their distance from the message start
-// (1 for the low byte of an LE word, 256 for the high byte), which makes a
-// sum over 16-byte aligned loads independent of the message's alignment.
-// Partial sums may be folded early: folding keeps the value mod 0xFFFF and
-// keeps it non-zero, so the final fold gives the reference's result.
-__device__ __forceinline__ uint32_t csum_dword(uint32_t x, uint32_t lo, uint32_t s0, uint32_t endb,
-					       bool odd)
+// Only whether the checksum is zero is kept (NSD_F_ICMP_BAD).  Sums run over
+// the 16-bit halves of 16-byte aligned loads with the bytes outside the
+// message masked off.  For a message at an odd address that weights every
+// byte by 256 relative to the reference's LE words, i.e. multiplies the sum
+// by 256 mod 0xFFFF (65536 = 1), so the folded sum is 0xFFFF exactly when the
+// reference's is (RFC 1071 byte-order independence) and the checksum is zero
+// exactly when the reference's is.  Partial sums may be folded early: folding
+// keeps the value mod 0xFFFF and keeps it non-zero.
+
+// byte mask of the dword at aligned position p for message bytes [s0, endb)
+__device__ __forceinline__ uint32_t msg_mask(uint32_t p, uint32_t s0, uint32_t endb)
 {
-	if (lo + 4 <= s0 || lo >= endb)
-		return 0;
-	if (lo < s0)
-		x &= 0xFFFFFFFFu << (8 * (s0 - lo));
-	if (lo + 4 > endb)
-		x &= 0xFFFFFFFFu >> (8 * (lo + 4 - endb));
-	const uint32_t ev = x & 0x00FF00FFu, od = (x >> 8) & 0x00FF00FFu;
-	const uint32_t e2 = (ev & 0xFFFF) + (ev >> 16), o2 = (od & 0xFFFF) + (od >> 16);
-	return odd ? (e2 << 8) + o2 : e2 + (o2 << 8);
+	uint32_t m = 0xFFFFFFFFu;
+	if (s0 > p)
+		m = s0 >= p + 4 ? 0u : m << (8 * (s0 - p));
+	if (endb < p + 4)
+		m = endb <= p ? 0u : m & (0xFFFFFFFFu >> (8 * (p + 4 - endb)));
+	return m;
 }
 
-__device__ __forceinline__ uint32_t csum_chunk(const uint4 &v, uint32_t lo, uint32_t s0, uint32_t endb,
-					       bool odd)
+// acc + low half + high half (v_sad_u16 against zero)
+__device__ __forceinline__ uint32_t sum_halves(uint32_t x, uint32_t acc)
 {
-	return csum_dword(v.x, lo, s0, endb, odd) + csum_dword(v.y, lo + 4, s0, endb, odd) +
-	       csum_dword(v.z, lo + 8, s0, endb, odd) + csum_dword(v.w, lo + 12, s0, endb, odd);
+	return __builtin_amdgcn_sad_u16(x, 0u, acc);
+}
+
+// chunk at aligned position lo, bytes outside [s0, endb) masked per lane
+__device__ __forceinline__ uint32_t csum_chunk(const uint4 &v, uint32_t lo, uint32_t s0, uint32_t endb)
+{
+	uint32_t acc = sum_halves(v.x & msg_mask(lo, s0, endb), 0u);
+	acc = sum_halves(v.y & msg_mask(lo + 4, s0, endb), acc);
+	acc = sum_halves(v.z & msg_mask(lo + 8, s0, endb), acc);
+	return sum_halves(v.w & msg_mask(lo + 12, s0, endb), acc);
+}
+
+// chunk j of a message: only chunk 0 and chunk nch - 1 can be partial, so
+// only their lanes take the masking path
+__device__ __forceinline__ uint32_t msg_chunk(const uint4 &v, uint32_t j, uint32_t s0, uint32_t endb,
+					      uint32_t nch, uint32_t acc)
+{
+	if (j == 0 || j == nch - 1)
+		return acc + csum_chunk(v, 16 * j, s0, endb);
+	acc = sum_halves(v.x, acc);
+	acc = sum_halves(v.y, acc);
+	acc = sum_halves(v.z, acc);
+	return sum_halves(v.w, acc);
 }
 
 __device__ __forceinline__ uint16_t csum_final(uint32_t sum)
@@ -273,19 +299,23 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v)
 }
 
 // Checksums of the messages the walks left pending (past the staged
-// window), wave-cooperatively: one message at a time per group slot, 64
-// lanes x 16 B = 1 KiB per coalesced load, four messages' loads in flight
-// together.  a = message start in `frames`, nbytes even (odd byte dropped).
+// window), wave-cooperatively: G messages at a time, 64 lanes x 16 B = 1 KiB
+// per coalesced load and message, the G loads in flight together; the G
+// per-lane partial sums are reduced across the wave by a transposing
+// butterfly (G - 1 + log2(64 / G) shuffles instead of 6 G).  a = message
+// start in `frames`, nbytes even (odd byte dropped).
+template <int G>
 __device__ __forceinline__ void wave_icmp_csums(const uint8_t *frames, bool pend, uint64_t a,
 						 uint32_t nbytes, uint8_t &flags, int lane)
 {
-	constexpr int G = 4;
+	static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "G must be a power of two <= 16");
 	uint64_t pm = __ballot(pend);
 	while (pm) {
 		int L[G];
-		uint32_t s0[G], endb[G], nch[G];
+		uint32_t sum[G], s0[G], endb[G], nch[G];
 		const uint4 *p[G];
 		uint4 v[G];
+		// all G first-round loads issued before any is used
 #pragma unroll
 		for (int t = 0; t < G; t++) {
 			L[t] = pm ? __ffsll((unsigned long long)pm) - 1 : -1;
@@ -304,15 +334,44 @@ __device__ __forceinline__ void wave_icmp_csums(const uint8_t *frames, bool pend
 		}
 #pragma unroll
 		for (int t = 0; t < G; t++) {
+			sum[t] = 0;
+			if (L[t] >= 0) {
+				sum[t] = msg_chunk(v[t], lane, s0[t], endb[t], nch[t], 0u);
+				for (uint32_t j = lane + 64; j < nch[t]; j += 64)   // messages over 1 KiB
+					sum[t] = msg_chunk(p[t][j], j, s0[t], endb[t], nch[t], sum[t]);
+				sum[t] = (sum[t] >> 16) + (sum[t] & 0xffff);
+			}
+		}
+		// transposing butterfly: after the step at distance d, a lane keeps
+		// half of its sums, each added to its partner's matching one
+		int k = G;
+#pragma unroll
+		for (int d = 32; d >= 1; d >>= 1) {
+			if (k > 1) {
+				const bool hi = lane & d;
+				k >>= 1;
+#pragma unroll
+				for (int t = 0; t < k; t++) {
+					const uint32_t mine = hi ? sum[t + k] : sum[t];
+					const uint32_t give = hi ? sum[t] : sum[t + k];
+					sum[t] = mine + __shfl_xor(give, d, 64);
+				}
+			} else {
+				sum[0] += __shfl_xor(sum[0], d, 64);
+			}
+		}
+		// message t's total sits in the lanes whose distance bits spell t
+#pragma unroll
+		for (int t = 0; t < G; t++) {
 			if (L[t] < 0)
 				break;
-			const bool odd = s0[t] & 1;
-			uint32_t sum = csum_chunk(v[t], 16 * lane, s0[t], endb[t], odd);
-			for (uint32_t j = lane + 64; j < nch[t]; j += 64)
-				sum += csum_chunk(p[t][j], 16 * j, s0[t], endb[t], odd);
-			sum = (sum >> 16) + (sum & 0xffff);
-			sum = wave_sum32(sum);
-			if (lane == L[t] && csum_final(sum))
+			int src = 0;
+#pragma unroll
+			for (int b = 0, d = 32; (1 << b) < G; b++, d >>= 1)
+				if (t & (G >> (b + 1)))
+					src |= d;
+			const uint32_t tot = __builtin_amdgcn_readlane(sum[0], src);
+			if (lane == L[t] && csum_final(tot))
 				flags |= NSD_F_ICMP_BAD;
 		}
 	}
@@ -392,13 +451,23 @@ __device__ __forceinline__ void block_flush(unsigned long long *s_cnt, unsigned 
 			atomicAdd(&counters[k], s_cnt[k]);
 }
 
+// Pending ICMPv4 checksums: entry = packet index | message offset << 32 |
+// message length << 48 (offsets and lengths are < 65536).  Block b keeps
+// PLISTS lists: one per pass-1 wave, then pass 2's.
+constexpr int PLISTS = WAVES + 1;
+
+__device__ __forceinline__ uint64_t pend_entry(uint32_t i, uint32_t off, uint32_t len)
+{
+	return (uint64_t)i | (uint64_t)(off & 0xFFFF) << 32 | (uint64_t)(len & 0xFFFF) << 48;
+}
+
 // ---- pass 1 ------------------------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void dissect_fast(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n,
 	int start_id, uint4 *__restrict__ rec, unsigned long long *__restrict__ counters,
 	uint32_t *__restrict__ queue, uint32_t region, uint32_t *__restrict__ qblk,
-	uint64_t *__restrict__ pend)
+	uint64_t *__restrict__ pend, uint32_t *__restrict__ pcnt)
 {
 	__shared__ uint32_t s_win[WAVES][64 * ROW];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
@@ -473,13 +542,12 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		}
 		wave_sync_lds();
 		if (MODE == PRINT_NORM) {
-			// ICMPv4 messages past the window: checksummed by the wave after
-			// the tile loop (their records are patched if the sum is bad)
+			// ICMPv4 messages past the window: listed for dissect_icmp, which
+			// patches the record if the sum is bad
 			const bool pnd = w.icmp_pend && !deferred;
 			const uint64_t pmask = __ballot(pnd);
 			if (pnd)
-				wq[npend + lanes_below(pmask)] = (uint64_t)i |
-					(uint64_t)(w.icmp_off | (w.icmp_len & 0xFFFF) << 8 | (w.n | w.flags) << 24) << 32;
+				wq[npend + lanes_below(pmask)] = pend_entry(i, w.icmp_off, w.icmp_len);
 			npend += (uint32_t)__popcll(pmask);
 		}
 
@@ -521,19 +589,8 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		d0 = d1;
 		d1 = d2;
 	}
-	// drain this wave's pending checksums (entries and records were written
-	// by this wave: its memory operations complete in order)
-	for (uint32_t k0 = 0; k0 < npend; k0 += 64) {
-		const bool on = k0 + lane < npend;
-		const uint64_t e = on ? wq[k0 + lane] : 0;
-		const uint32_t i = (uint32_t)e, meta = (uint32_t)(e >> 32);
-		const uint64_t off = on ? NSD_DESC_OFF(desc[i]) : 0;
-		uint8_t fl = 0;
-		wave_icmp_csums(frames, on, off + (meta & 0xFF), (meta >> 8) & 0xFFFEu, fl, lane);
-		if (fl)
-			((uint8_t *)rec)[(size_t)i * 16 + 10] = (uint8_t)(meta >> 24) | NSD_F_ICMP_BAD;
-		fc.icmpbad += FlagCnt::pc(fl != 0);
-	}
+	if (lane == 0)
+		pcnt[blockIdx.x * PLISTS + wv] = npend;
 	fc.flush(s_cnt, lane);
 	block_flush(s_cnt, counters);
 	if (threadIdx.x == 0)
@@ -546,15 +603,20 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, int start_id,
 	uint4 *__restrict__ rec, nsd_ext *__restrict__ ext, uint32_t ext_cap,
 	uint32_t *__restrict__ ext_count, unsigned long long *__restrict__ counters,
-	const uint32_t *__restrict__ queue, uint32_t region, const uint32_t *__restrict__ qblk)
+	const uint32_t *__restrict__ queue, uint32_t region, const uint32_t *__restrict__ qblk,
+	uint64_t *__restrict__ pend2, uint32_t *__restrict__ pcnt)
 {
 	__shared__ uint32_t s_win[WAVES][64 * ROW];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
 	__shared__ uint8_t s_lay3[256];
+	__shared__ uint32_t s_pn;
 
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
+	if (threadIdx.x == 0)
+		s_pn = 0;
 	block_init(s_cnt, s_lay3);
+	uint64_t *const bp = pend2 + (size_t)blockIdx.x * region;   // this block's pending list
 
 	// block b drains the queue region pass 1's block b filled
 	const uint32_t nq = qblk[blockIdx.x];
@@ -596,8 +658,18 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 			if (susp)
 				wb = (w.data + m) & ~15u;
 		}
-		if (MODE == PRINT_NORM)
-			wave_icmp_csums(frames, w.icmp_pend, off + w.icmp_off, w.icmp_len & ~1u, w.flags, lane);
+		if (MODE == PRINT_NORM) {
+			const uint64_t pm = __ballot(w.icmp_pend);
+			if (pm) {
+				const int leader = __ffsll((unsigned long long)pm) - 1;
+				uint32_t pb = 0;
+				if (lane == leader)
+					pb = atomicAdd(&s_pn, (uint32_t)__popcll(pm));
+				pb = __shfl(pb, leader, 64);
+				if (w.icmp_pend)
+					bp[pb + lanes_below(pm)] = pend_entry(i, w.icmp_off, w.icmp_len);
+			}
+		}
 		if (!valid)
 			continue;
 		if (w.ext_on) {
@@ -610,6 +682,64 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	}
 	fc.flush(s_cnt, lane);
 	block_flush(s_cnt, counters);
+	if (threadIdx.x == 0)
+		pcnt[blockIdx.x * PLISTS + WAVES] = s_pn;   // ordered by block_flush's barrier
+}
+
+// ---- pending ICMPv4 checksums -------------------------------------------------
+// Runs after both passes (the records are final): block b's waves take b's
+// lists, G messages' loads in flight per wave, and patch the flags byte of
+// the records whose sum is bad.
+constexpr uint32_t SMALL_CHUNKS = 6;
+
+template <int G>
+__global__ __launch_bounds__(BLOCK) void dissect_icmp(
+	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint4 *__restrict__ rec,
+	unsigned long long *__restrict__ counters, const uint64_t *__restrict__ pend,
+	const uint64_t *__restrict__ pend2, uint32_t region, const uint32_t *__restrict__ pcnt)
+{
+	const int lane = threadIdx.x & 63;
+	const int wv = threadIdx.x >> 6;
+	uint32_t bad = 0;
+	for (int l = 0; l < PLISTS; l++) {
+		const uint32_t cnt = pcnt[blockIdx.x * PLISTS + l];
+		const uint64_t *list = l < WAVES ? pend + ((size_t)blockIdx.x * WAVES + l) * (region / WAVES)
+						 : pend2 + (size_t)blockIdx.x * region;
+		// the block's waves split each list in 64-entry pieces
+		for (uint32_t k0 = 64 * ((wv + l) % WAVES); k0 < cnt; k0 += 64 * WAVES) {
+			const bool on = k0 + lane < cnt;
+			const uint64_t e = on ? list[k0 + lane] : 0;
+			const uint32_t i = (uint32_t)e;
+			const uint32_t moff = (uint32_t)(e >> 32) & 0xFFFF, mlen = (uint32_t)(e >> 48);
+			const uint64_t a = (on ? NSD_DESC_OFF(desc[i]) : 0) + moff;
+			const uint32_t nb = mlen & ~1u;
+			// short messages (the 64 B frames of a mix): one lane each;
+			// longer ones: the whole wave per message
+			const bool small = on && (a & 15) + nb <= 16 * SMALL_CHUNKS;
+			uint8_t fl = 0;
+			if (__ballot(small)) {
+				if (small) {
+					const uint4 *p = (const uint4 *)(frames + (a & ~15ull));
+					const uint32_t s0 = (uint32_t)(a & 15), endb = s0 + nb;
+					uint32_t sum = 0;
+#pragma unroll
+					for (uint32_t j = 0; j < SMALL_CHUNKS; j++)
+						if (16 * j < endb)
+							sum += csum_chunk(p[j], 16 * j, s0, endb);
+					if (csum_final(sum))
+						fl = NSD_F_ICMP_BAD;
+				}
+			}
+			wave_icmp_csums<G>(frames, on && !small, a, nb, fl, lane);
+			if (fl) {
+				uint8_t *nf = (uint8_t *)rec + (size_t)i * 16 + 10;
+				*nf = *nf | NSD_F_ICMP_BAD;
+			}
+			bad += FlagCnt::pc(fl != 0);
+		}
+	}
+	if (lane == 0 && bad)
+		atomicAdd(&counters[NSD_CNT_ICMP_BAD], (unsigned long long)bad);
 }
 
 } // namespace nsd
@@ -633,10 +763,11 @@ static size_t region_slots(uint32_t n)
 	return ((size_t)n + (size_t)NSD_MAX_GRID * nsd::BLOCK + 1) & ~(size_t)1;
 }
 
+// workspace: qblk[NSD_MAX_GRID], pcnt[NSD_MAX_GRID * 8], the deferral queue
+// (u32 per slot), the pass-1 and pass-2 pending-checksum lists (u64 per slot)
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
-	// qblk, the deferral queue (u32 per slot), the pending-checksum lists (u64 per slot)
-	return 4 * (size_t)NSD_MAX_GRID + 4 * region_slots(n) + 8 * region_slots(n);
+	return 4 * (size_t)NSD_MAX_GRID * 9 + (4 + 8 + 8) * region_slots(n);
 }
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
@@ -679,26 +810,30 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	unsigned long long *cnt = (unsigned long long *)d_counters;
 	uint4 *rec = (uint4 *)d_rec;
 	uint32_t *qblk = (uint32_t *)d_ws;
-	uint32_t *queue = qblk + NSD_MAX_GRID;
+	uint32_t *pcnt = qblk + NSD_MAX_GRID;
+	uint32_t *queue = pcnt + 8 * NSD_MAX_GRID;
 	uint64_t *pend = (uint64_t *)(queue + region_slots(n));
+	uint64_t *pend2 = pend + region_slots(n);
 	switch (mode) {
 	case PRINT_NORM:
 		hipLaunchKernelGGL(dissect_fast<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend);
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend, pcnt);
 		hipLaunchKernelGGL(dissect_general<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
-				   region, qblk);
+				   region, qblk, pend2, pcnt);
+		hipLaunchKernelGGL(dissect_icmp<NSD_DRAIN_G>, dim3(blocks), dim3(BLOCK), 0, stream,
+				   d_frames, d_desc, rec, cnt, pend, pend2, region, pcnt);
 		break;
 	case PRINT_LESS:
 		hipLaunchKernelGGL(dissect_fast<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend);
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend, pcnt);
 		hipLaunchKernelGGL(dissect_general<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
-				   region, qblk);
+				   region, qblk, pend2, pcnt);
 		break;
 	default:
 		hipLaunchKernelGGL(dissect_fast<PRINT_HEX>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend);
+				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend, pcnt);
 		break;
 	}
 	return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -1,0 +1,249 @@
+// nsd_pipe.cpp - pipelined host-batch path (include/netsniff_dissect.h,
+// nsd_pipe_*): the capture side of SURVEY 8f.2.  A batch (one TPACKET_V3
+// block, walk_t3_block netsniff-ng.c:991-1039, or a run of pcap records,
+// read_pcap netsniff-ng.c:700-760) goes H2D, through the dissect kernels and
+// D2H on its own stream slot; `depth` slots rotate, so batch k's copies
+// overlap batch k+1's walk and the H2D / D2H engines run concurrently.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/netsniff_dissect.h"
+
+extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
+				  int start_id, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+				  void *d_ws, int grid, hipStream_t stream);
+extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
+int nsd_start_for(int linktype);
+
+namespace {
+constexpr int MAX_DEPTH = 8;
+
+bool ok(hipError_t e, const char *what)
+{
+	if (e != hipSuccess) {
+		fprintf(stderr, "netsniff-dissect pipe: %s: %s\n", what, hipGetErrorString(e));
+		return false;
+	}
+	return true;
+}
+
+struct Slot {
+	hipStream_t stream = nullptr;
+	hipEvent_t done = nullptr;
+	uint8_t *frames = nullptr;
+	uint64_t *desc = nullptr;
+	nsd_rec *rec = nullptr;
+	nsd_ext *ext = nullptr;
+	uint32_t *small = nullptr;   // ext_count at +0, counters at +64 (device)
+	uint64_t *small_h = nullptr; // pinned host copy of the same 576 bytes
+	void *ws = nullptr;
+	// the batch in flight
+	bool busy = false;
+	int status = NSD_OK;
+	uint32_t n = 0;
+	nsd_ext *ext_out = nullptr;
+	uint32_t *ext_count_out = nullptr;
+	uint64_t *counters_out = nullptr;
+	int *status_out = nullptr;
+};
+} // namespace
+
+struct nsd_pipe {
+	uint32_t max_pkts = 0;
+	size_t max_bytes = 0;
+	uint32_t ext_cap = 0;
+	int depth = 0;
+	int start_id = 0;
+	int mode = 0;
+	int head = 0;    // oldest in flight
+	int count = 0;   // in flight
+	Slot slot[MAX_DEPTH];
+};
+
+static void slot_free(Slot &s)
+{
+	if (s.stream) (void)hipStreamDestroy(s.stream);
+	if (s.done) (void)hipEventDestroy(s.done);
+	if (s.frames) (void)hipFree(s.frames);
+	if (s.desc) (void)hipFree(s.desc);
+	if (s.rec) (void)hipFree(s.rec);
+	if (s.ext) (void)hipFree(s.ext);
+	if (s.small) (void)hipFree(s.small);
+	if (s.small_h) (void)hipHostFree(s.small_h);
+	if (s.ws) (void)hipFree(s.ws);
+	s = Slot();
+}
+
+extern "C" void nsd_pipe_destroy(nsd_pipe *p)
+{
+	if (!p)
+		return;
+	nsd_pipe_drain(p);
+	for (int k = 0; k < p->depth; k++)
+		slot_free(p->slot[k]);
+	delete p;
+}
+
+extern "C" nsd_pipe *nsd_pipe_create(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_cap,
+				     int depth, int linktype, int mode)
+{
+	if (!max_pkts || !max_frame_bytes || depth < 1 || depth > MAX_DEPTH || mode < PRINT_NORM ||
+	    mode > PRINT_NONE)
+		return nullptr;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+		return nullptr;
+	nsd_pipe *p = new nsd_pipe;
+	p->max_pkts = max_pkts;
+	p->max_bytes = max_frame_bytes;
+	p->ext_cap = ext_cap;
+	p->depth = depth;
+	p->start_id = nsd_start_for(linktype);
+	p->mode = mode;
+	for (int k = 0; k < depth; k++) {
+		Slot &s = p->slot[k];
+		bool good = ok(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream") &&
+			    ok(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "event") &&
+			    ok(hipMalloc(&s.frames, max_frame_bytes + NSD_FRAME_PAD), "hipMalloc") &&
+			    ok(hipMalloc(&s.desc, (size_t)max_pkts * 8), "hipMalloc") &&
+			    ok(hipMalloc(&s.rec, (size_t)max_pkts * sizeof(nsd_rec)), "hipMalloc") &&
+			    (!ext_cap || ok(hipMalloc(&s.ext, (size_t)ext_cap * sizeof(nsd_ext)), "hipMalloc")) &&
+			    ok(hipMalloc(&s.small, 64 + NSD_NCOUNTERS * 8), "hipMalloc") &&
+			    ok(hipHostMalloc(&s.small_h, 64 + NSD_NCOUNTERS * 8, hipHostMallocDefault), "hipHostMalloc") &&
+			    ok(hipMalloc(&s.ws, nsd_launch_workspace_bytes(max_pkts)), "hipMalloc");
+		if (!good) {
+			nsd_pipe_destroy(p);
+			return nullptr;
+		}
+	}
+	return p;
+}
+
+// complete the oldest batch
+static int complete_oldest(nsd_pipe *p)
+{
+	Slot &s = p->slot[p->head];
+	int st = s.status;
+	if (st == NSD_OK && !ok(hipEventSynchronize(s.done), "batch"))
+		st = NSD_ERR_HIP;
+	if (st == NSD_OK) {
+		const uint32_t used = (uint32_t)s.small_h[0];
+		if (s.counters_out)
+			memcpy(s.counters_out, s.small_h + 8, NSD_NCOUNTERS * 8);
+		if (s.ext_count_out)
+			*s.ext_count_out = used;
+		const uint32_t k = used < p->ext_cap ? used : p->ext_cap;
+		if (k && s.ext_out &&
+		    !ok(hipMemcpyAsync(s.ext_out, s.ext, (size_t)k * sizeof(nsd_ext), hipMemcpyDeviceToHost,
+				       s.stream), "ext D2H"))
+			st = NSD_ERR_HIP;
+		if (k && s.ext_out && st == NSD_OK && !ok(hipStreamSynchronize(s.stream), "ext D2H"))
+			st = NSD_ERR_HIP;
+	}
+	if (s.status_out)
+		*s.status_out = st;
+	s.busy = false;
+	p->head = (p->head + 1) % p->depth;
+	p->count--;
+	return st;
+}
+
+extern "C" int nsd_pipe_wait(nsd_pipe *p)
+{
+	if (!p)
+		return NSD_ERR_ARG;
+	if (!p->count)
+		return 1;
+	return complete_oldest(p);
+}
+
+extern "C" int nsd_pipe_drain(nsd_pipe *p)
+{
+	if (!p)
+		return NSD_ERR_ARG;
+	int st = NSD_OK;
+	while (p->count) {
+		int r = complete_oldest(p);
+		if (r != NSD_OK && st == NSD_OK)
+			st = r;
+	}
+	return st;
+}
+
+extern "C" int nsd_pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
+			       const nsd_desc_t *desc, uint32_t n, nsd_rec *rec, nsd_ext *ext,
+			       uint32_t *ext_count, uint64_t *counters, int *status)
+{
+	if (!p || (n && (!frames || !desc || !rec)) || (p->ext_cap && !ext && n))
+		return NSD_ERR_ARG;
+	if (n > p->max_pkts || frames_len > p->max_bytes)
+		return NSD_ERR_ARG;
+	for (uint32_t i = 0; i < n; i++) {
+		const uint64_t cap = NSD_DESC_CAPLEN(desc[i]);
+		if (cap > NSD_MAX_CAPLEN)
+			return NSD_ERR_CAPLEN;
+		if (NSD_DESC_OFF(desc[i]) + cap > frames_len)
+			return NSD_ERR_ARG;
+	}
+	if (p->count == p->depth)
+		complete_oldest(p);   // its status goes to its own *status
+	const int k = (p->head + p->count) % p->depth;
+	Slot &s = p->slot[k];
+	s.busy = true;
+	s.n = n;
+	s.ext_out = ext;
+	s.ext_count_out = ext_count;
+	s.counters_out = counters;
+	s.status_out = status;
+	s.status = NSD_OK;
+	p->count++;
+	const hipStream_t st = s.stream;
+	bool good = ok(hipMemsetAsync(s.small, 0, 64 + NSD_NCOUNTERS * 8, st), "memset");
+	if (good && n) {
+		good = ok(hipMemcpyAsync(s.frames, frames, frames_len, hipMemcpyHostToDevice, st), "H2D") &&
+		       ok(hipMemsetAsync(s.frames + frames_len, 0, NSD_FRAME_PAD, st), "memset") &&
+		       ok(hipMemcpyAsync(s.desc, desc, (size_t)n * 8, hipMemcpyHostToDevice, st), "H2D");
+		good = good && nsd_launch_dissect(s.frames, s.desc, n, p->start_id, p->mode, s.rec,
+						  p->ext_cap ? s.ext : nullptr, p->ext_cap, s.small,
+						  (uint64_t *)((uint8_t *)s.small + 64), s.ws, 0, st) == 0;
+		good = good && ok(hipMemcpyAsync(rec, s.rec, (size_t)n * sizeof(nsd_rec), hipMemcpyDeviceToHost,
+						 st), "D2H");
+	}
+	good = good && ok(hipMemcpyAsync(s.small_h, s.small, 64 + NSD_NCOUNTERS * 8, hipMemcpyDeviceToHost,
+					 st), "D2H") &&
+	       ok(hipEventRecord(s.done, st), "event");
+	if (!good)
+		s.status = NSD_ERR_HIP;
+	return good ? NSD_OK : NSD_ERR_HIP;
+}
+
+extern "C" void *nsd_host_alloc(size_t len)
+{
+	void *p = nullptr;
+	if (!len || hipHostMalloc(&p, len, hipHostMallocDefault) != hipSuccess)
+		return nullptr;
+	return p;
+}
+
+extern "C" void nsd_host_free(void *ptr)
+{
+	if (ptr)
+		(void)hipHostFree(ptr);
+}
+
+extern "C" int nsd_host_register(void *ptr, size_t len)
+{
+	if (!ptr || !len)
+		return NSD_ERR_ARG;
+	return hipHostRegister(ptr, len, hipHostRegisterDefault) == hipSuccess ? NSD_OK : NSD_ERR_HIP;
+}
+
+extern "C" int nsd_host_unregister(void *ptr)
+{
+	if (!ptr)
+		return NSD_ERR_ARG;
+	return hipHostUnregister(ptr) == hipSuccess ? NSD_OK : NSD_ERR_HIP;
+}

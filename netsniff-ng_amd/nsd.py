@@ -37,7 +37,9 @@ OPS_NAMES = ["invalid", "ethernet", "vlan", "QinQ", "mpls_uc", "arp", "lldp", "i
 ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup_all",
                "dissector_set_print_type", "nsd_dissect_device", "dissector_entry_batch",
                "nsd_workspace_bytes", "nsd_dissect_device_ws", "nsd_format_packet", "nsd_lookup_init", "nsd_lookup_cleanup", "nsd_tprintf_wrap",
-               "nsd_version", "nsd_device_count"]
+               "nsd_version", "nsd_device_count", "nsd_pipe_create", "nsd_pipe_submit",
+               "nsd_pipe_wait", "nsd_pipe_drain", "nsd_pipe_destroy", "nsd_host_alloc",
+               "nsd_host_free", "nsd_host_register", "nsd_host_unregister"]
 
 _lib = None
 _vp, _u32, _u64, _int, _sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
@@ -81,6 +83,24 @@ def lib():
                                        ctypes.c_char_p, _sz]
         L.nsd_version.restype = ctypes.c_char_p
         L.nsd_device_count.restype = _int
+        L.nsd_pipe_create.restype = _vp
+        L.nsd_pipe_create.argtypes = [_u32, _sz, _u32, _int, _int, _int]
+        L.nsd_pipe_submit.restype = _int
+        L.nsd_pipe_submit.argtypes = [_vp, _vp, _sz, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
+        L.nsd_pipe_wait.restype = _int
+        L.nsd_pipe_wait.argtypes = [_vp]
+        L.nsd_pipe_drain.restype = _int
+        L.nsd_pipe_drain.argtypes = [_vp]
+        L.nsd_pipe_destroy.restype = None
+        L.nsd_pipe_destroy.argtypes = [_vp]
+        L.nsd_host_alloc.restype = _vp
+        L.nsd_host_alloc.argtypes = [_sz]
+        L.nsd_host_free.restype = None
+        L.nsd_host_free.argtypes = [_vp]
+        L.nsd_host_register.restype = _int
+        L.nsd_host_register.argtypes = [_vp, _sz]
+        L.nsd_host_unregister.restype = _int
+        L.nsd_host_unregister.argtypes = [_vp]
         L.dissector_init_all.argtypes = [_int]
         L.dissector_entry_point.argtypes = [_vp, _sz, _int, _int, _vp]
         _lib = L
@@ -148,6 +168,52 @@ def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_cap
                                      cnt.ctypes.data, counters.ctypes.data)
     _check(rc, "dissector_entry_batch")
     return rec, ext[:min(int(cnt[0]), ext_cap)], counters
+
+
+class Pipe:
+    """Pipelined host-batch path (nsd_pipe_*): submit numpy batches, records
+    land in the caller's arrays when the batch completes.  Arrays passed to
+    submit() are kept alive until then."""
+
+    def __init__(self, max_pkts, max_frame_bytes, ext_cap=0, depth=3, mode=PRINT_NORM,
+                 linktype=LINKTYPE_EN10MB):
+        self.L = lib()
+        self.p = self.L.nsd_pipe_create(max_pkts, max_frame_bytes, ext_cap, depth, linktype, mode)
+        if not self.p:
+            raise NsdError("nsd_pipe_create failed")
+        self.ext_cap = ext_cap
+        self.depth = depth
+        self.inflight = []
+
+    def submit(self, frames, desc, rec, ext=None, ext_count=None, counters=None, status=None):
+        n = len(desc)
+        ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+        rc = self.L.nsd_pipe_submit(self.p, frames.ctypes.data, frames.nbytes, desc.ctypes.data, n,
+                                    rec.ctypes.data, ptr(ext), ptr(ext_count), ptr(counters),
+                                    ptr(status))
+        _check(rc, "nsd_pipe_submit")
+        self.inflight.append((frames, desc, rec, ext, ext_count, counters, status))
+        if len(self.inflight) > self.depth:   # the library completed the oldest first
+            self.inflight.pop(0)
+
+    def wait(self):
+        rc = self.L.nsd_pipe_wait(self.p)
+        if self.inflight:
+            self.inflight.pop(0)
+        return rc
+
+    def drain(self):
+        rc = self.L.nsd_pipe_drain(self.p)
+        self.inflight.clear()
+        return rc
+
+    def close(self):
+        if self.p:
+            self.L.nsd_pipe_destroy(self.p)
+            self.p = None
+
+    def __del__(self):
+        self.close()
 
 
 def format_batch(frames, desc, rec, ext=None, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB):

@@ -116,3 +116,33 @@ def test_ext_table_full():
             holders += 1
             assert _chain(rec, ext, i) == _chain(orec, oext, i)
     assert holders == 1
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_pipe_batches(depth):
+    """The pipelined host-batch path (nsd_pipe_*): batches of different
+    sizes and configs in flight together; every batch's records, ext and
+    counters equal the oracle's for that batch."""
+    specs = [(T.SYN_IMIX, 20000, 0), (T.SYN_IPV6X, 7000, 0), (T.SYN_UDP64, 1, 5),
+             (T.SYN_IMIX, 15000, 20000), (T.SYN_IPV6X, 9000, 7000), (T.SYN_IMIX, 3, 99)]
+    batches = [T.make_batch(cfg, n, lo=lo) for cfg, n, lo in specs]
+    max_pkts = max(len(d) for _, d in batches)
+    max_bytes = max(f.nbytes for f, _ in batches)
+    pipe = nsd.Pipe(max_pkts, max_bytes, ext_cap=max_pkts, depth=depth)
+    outs = []
+    for frames, desc in batches:
+        rec = np.zeros(len(desc), dtype=nsd.REC_DTYPE)
+        ext = np.zeros(max_pkts, dtype=nsd.EXT_DTYPE)
+        ec = np.zeros(1, np.uint32)
+        cnt = np.zeros(nsd.NCOUNTERS, np.uint64)
+        st = np.full(1, -99, np.int32)
+        pipe.submit(frames, desc, rec, ext, ec, cnt, st)
+        outs.append((rec, ext, ec, cnt, st))
+    assert pipe.drain() == 0
+    for (frames, desc), (rec, ext, ec, cnt, st) in zip(batches, outs):
+        assert st[0] == 0
+        orec, oext, ocnt, _ = T.oracle_records(frames, desc)
+        assert_same_records(rec, orec, ext[:int(ec[0])], oext)
+        assert np.array_equal(cnt, ocnt)
+    assert pipe.wait() == 1
+    pipe.close()
