@@ -72,6 +72,60 @@ def cpu_baseline(cfg, n_sample, threads, seconds):
     return done / dt / 1e6, done, dt
 
 
+def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
+    """Host memory in, records in host memory out: `nbatch`
+    batches of `batch` packets from one pinned host buffer go through the
+    pipelined path (nsd_pipe_*: H2D, dissect kernels, D2H of records, ext and
+    counters, `depth` batches in flight).  Returns a dict for the JSON line."""
+    L = nsd.lib()
+    n = batch * nbatch
+    frames, desc = T.make_batch(cfg, n, lo=0, threads=16)
+    off = (desc & np.uint64((1 << 40) - 1)).astype(np.int64)
+    cap = (desc >> np.uint64(40)).astype(np.int64)
+    rec = np.zeros(n, dtype=nsd.REC_DTYPE)
+    pinned = [a for a in (frames, rec) if L.nsd_host_register(a.ctypes.data, a.nbytes) == 0]
+    slices = []
+    for k in range(nbatch):
+        a, b = k * batch, (k + 1) * batch
+        lo, hi = int(off[a]), int(off[b - 1] + cap[b - 1])
+        d = (desc[a:b] - np.uint64(lo)).astype(np.uint64)
+        slices.append((frames[lo:hi + nsd.FRAME_PAD], d, rec[a:b]))
+    descs_pinned = [L.nsd_host_register(d.ctypes.data, d.nbytes) == 0 for _, d, _ in slices]
+    max_bytes = max(f.nbytes for f, _, _ in slices)
+    ext_cap = batch if cfg == T.SYN_IPV6X else max(batch // 64, 4096)
+    pipe = nsd.Pipe(batch, max_bytes, ext_cap=ext_cap, depth=depth, mode=mode)
+    exts = [np.zeros(ext_cap, dtype=nsd.EXT_DTYPE) for _ in range(depth + 1)]
+    cnts = np.zeros((nbatch, nsd.NCOUNTERS), np.uint64)
+    ecs = np.zeros(nbatch, np.uint32)
+    sts = np.zeros(nbatch, np.int32)
+    times = []
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        for k, (f, d, rr) in enumerate(slices):
+            pipe.submit(f, d, rr, exts[k % (depth + 1)], ecs[k:k + 1], cnts[k], sts[k:k + 1])
+        assert pipe.drain() == 0
+        dt = time.perf_counter() - t0
+        if r:
+            times.append(dt)
+    pipe.close()
+    assert int(cnts[:, nsd.CNT_PKTS].sum()) == n and not sts.any()
+    h2d = sum(f.nbytes - nsd.FRAME_PAD + d.nbytes for f, d, _ in slices)
+    d2h = n * REC_B
+    dt = min(times)
+    for a in pinned:
+        L.nsd_host_unregister(a.ctypes.data)
+    for ok, (_, d, _) in zip(descs_pinned, slices):
+        if ok:
+            L.nsd_host_unregister(d.ctypes.data)
+    return {"value": round(n / dt / 1e6, 2), "unit": "Mpkt/s",
+            "pcie_gbs": round((h2d + d2h) / dt / 1e9, 2),
+            "h2d_bytes_per_pkt": round(h2d / n, 2), "d2h_bytes_per_pkt": REC_B,
+            "batches": nbatch, "batch_packets": batch, "depth": depth,
+            "pinned": len(pinned) == 2 and all(descs_pinned),
+            "note": "host frames -> H2D -> dissect kernels -> D2H records/ext/counters "
+                    "(nsd_pipe_*), best of %d passes" % reps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -84,6 +138,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="packets in the CPU sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline duration")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end pass")
+    ap.add_argument("--e2e-batch", type=int, default=1 << 20)
+    ap.add_argument("--e2e-batches", type=int, default=16)
+    ap.add_argument("--e2e-depth", type=int, default=3)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,6 +256,10 @@ def main():
                          f" walk (oracle/nsd_oracle.c), {threads} threads; 1 thread:"
                          f" {v1:.3f} Mpkt/s ({p1} packets, {d1:.1f} s)"}
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = end_to_end(c["cfg"], args.e2e_batch, args.e2e_batches, args.e2e_depth, args.mode)
+
     if rank == 0:
         out = {
             "metric": "Mpkt/s device-resident dissect (bit-exact fields vs ref)",
@@ -212,6 +274,7 @@ def main():
             "gbps_frames": round(frame_bytes * world * args.steps / elapsed / 1e9, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
         }
         print(json.dumps(out))
     if dist is not None:
