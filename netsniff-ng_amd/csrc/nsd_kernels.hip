@@ -597,6 +597,50 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		qblk[blockIdx.x] = s_qn;   // block_flush's barrier ordered every append before this
 }
 
+// Block end of pass 2: the block's scratch ext entries move to the caller's
+// table at a range taken with one global atomic (so the table stays compact:
+// entries [0, min(count, cap)) are filled), and each owner record gets its
+// final slot (bytes 10..15: nflags, slot).  Entries past the capacity leave
+// their record with NSD_F_OVERFLOW and slot 0xFFFFFFFF.  Only the used
+// dwords of an entry are copied, 16 lanes per entry.
+__device__ __forceinline__ void ext_compact(const nsd_ext *scr, uint32_t &s_en, uint32_t &s_ebase,
+					    uint4 *rec, nsd_ext *ext, uint32_t ext_cap,
+					    uint32_t *ext_count, unsigned long long *counters)
+{
+	__syncthreads();
+	if (threadIdx.x == 0)
+		s_ebase = s_en ? atomicAdd(ext_count, s_en) : 0u;
+	__syncthreads();
+	const uint32_t ne = s_en, base = s_ebase;
+	const uint32_t t = threadIdx.x & 15;
+	uint32_t ovf = 0;
+	for (uint32_t j = threadIdx.x >> 4; j < ne; j += BLOCK / 16) {
+		const uint32_t *src = (const uint32_t *)(scr + j);
+		const uint32_t h1 = src[1];
+		const uint32_t nl = h1 & 0xFFFF, nf = h1 >> 16;
+		const uint32_t slot = base + j;
+		const bool fits = slot < ext_cap;
+		if (fits) {
+			uint32_t *dst = (uint32_t *)(ext + slot);
+			const uint32_t idw = 2 + (nl + 3) / 4, offw = 18 + (nl + 1) / 2;
+			for (uint32_t x = t; x < sizeof(nsd_ext) / 4; x += 16) {
+				if (x < idw || (x >= 18 && x < offw))
+					dst[x] = x == 1 ? nl : src[x];
+			}
+		}
+		if (t == 0) {
+			const uint32_t s = fits ? slot : 0xFFFFFFFFu;
+			const uint32_t f = fits ? nf : nf | NSD_F_OVERFLOW;
+			uint8_t *r = (uint8_t *)(rec + src[0]);
+			*(uint16_t *)(r + 10) = (uint16_t)((f & 0xFF) | (s & 0xFF) << 8);
+			*(uint32_t *)(r + 12) = s >> 8;
+			ovf += !fits && !(nf & NSD_F_OVERFLOW);
+		}
+	}
+	if (t == 0 && ovf)
+		atomicAdd(&counters[NSD_CNT_OVERFLOW], (unsigned long long)ovf);
+}
+
 // ---- pass 2 ------------------------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void dissect_general(
@@ -604,17 +648,19 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	uint4 *__restrict__ rec, nsd_ext *__restrict__ ext, uint32_t ext_cap,
 	uint32_t *__restrict__ ext_count, unsigned long long *__restrict__ counters,
 	const uint32_t *__restrict__ queue, uint32_t region, const uint32_t *__restrict__ qblk,
-	uint64_t *__restrict__ pend2, uint32_t *__restrict__ pcnt)
+	uint64_t *__restrict__ pend2, uint32_t *__restrict__ pcnt, nsd_ext *__restrict__ scratch)
 {
 	__shared__ uint32_t s_win[WAVES][64 * ROW];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
 	__shared__ uint8_t s_lay3[256];
-	__shared__ uint32_t s_pn;
+	__shared__ uint32_t s_pn, s_en, s_ebase;
 
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
-	if (threadIdx.x == 0)
+	if (threadIdx.x == 0) {
 		s_pn = 0;
+		s_en = 0;
+	}
 	block_init(s_cnt, s_lay3);
 	uint64_t *const bp = pend2 + (size_t)blockIdx.x * region;   // this block's pending list
 
@@ -622,7 +668,8 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	const uint32_t nq = qblk[blockIdx.x];
 	const uint32_t *const bq = queue + (size_t)blockIdx.x * region;
 	const WaveCnt wc{ s_cnt };
-	const ExtSink es{ ext, ext_cap, ext_count };
+	nsd_ext *const scr = scratch + (size_t)blockIdx.x * region;   // this block's ext scratch
+	const ExtSink es{ scr, &s_en };
 	FlagCnt fc;
 
 	for (uint32_t base = wv * 64; base < nq; base += BLOCK) {
@@ -673,9 +720,10 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 		if (!valid)
 			continue;
 		if (w.ext_on) {
-			nsd_ext *e = ext + w.slot;
+			nsd_ext *e = scr + w.slot;
 			e->pkt = i;
 			e->nlayers = (uint16_t)(w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS);
+			e->rsvd = (uint16_t)(NSD_N_EXT | w.flags);   // the record's nflags, for ext_compact
 		}
 		rec[i] = pack_record(w);
 		fc.add(w, caplen, true);
@@ -684,6 +732,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	block_flush(s_cnt, counters);
 	if (threadIdx.x == 0)
 		pcnt[blockIdx.x * PLISTS + WAVES] = s_pn;   // ordered by block_flush's barrier
+	ext_compact(scr, s_en, s_ebase, rec, ext, ext_cap, ext_count, counters);
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
@@ -764,10 +813,11 @@ static size_t region_slots(uint32_t n)
 }
 
 // workspace: qblk[NSD_MAX_GRID], pcnt[NSD_MAX_GRID * 8], the deferral queue
-// (u32 per slot), the pass-1 and pass-2 pending-checksum lists (u64 per slot)
+// (u32 per slot), the pass-1 and pass-2 pending-checksum lists (u64 per slot),
+// pass 2's per-block ext scratch (nsd_ext per slot, 8-byte aligned)
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
-	return 4 * (size_t)NSD_MAX_GRID * 9 + (4 + 8 + 8) * region_slots(n);
+	return 4 * (size_t)NSD_MAX_GRID * 9 + (4 + 8 + 8 + sizeof(nsd_ext)) * region_slots(n);
 }
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
@@ -814,13 +864,14 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	uint32_t *queue = pcnt + 8 * NSD_MAX_GRID;
 	uint64_t *pend = (uint64_t *)(queue + region_slots(n));
 	uint64_t *pend2 = pend + region_slots(n);
+	nsd_ext *scratch = (nsd_ext *)(pend2 + region_slots(n));
 	switch (mode) {
 	case PRINT_NORM:
 		hipLaunchKernelGGL(dissect_fast<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend, pcnt);
 		hipLaunchKernelGGL(dissect_general<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
-				   region, qblk, pend2, pcnt);
+				   region, qblk, pend2, pcnt, scratch);
 		hipLaunchKernelGGL(dissect_icmp<NSD_DRAIN_G>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, rec, cnt, pend, pend2, region, pcnt);
 		break;
@@ -829,7 +880,7 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend, pcnt);
 		hipLaunchKernelGGL(dissect_general<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
-				   region, qblk, pend2, pcnt);
+				   region, qblk, pend2, pcnt, scratch);
 		break;
 	default:
 		hipLaunchKernelGGL(dissect_fast<PRINT_HEX>, dim3(blocks), dim3(BLOCK), 0, stream,

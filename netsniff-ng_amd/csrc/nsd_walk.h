@@ -69,12 +69,16 @@ struct WalkOut {
 	uint32_t icmp_off, icmp_len;
 };
 
-// Ext spill: the first time a packet needs the ext form it takes a slot and
-// copies the layers collected so far; later layers go straight to the slot.
+// Ext spill: the first time a packet needs the ext form it takes a slot in
+// its block's scratch table (LDS counter, one add per group of lanes reaching
+// that point together) and copies the layers collected so far; later layers
+// go straight to the slot.  The block compacts its scratch entries into the
+// caller's ext table when it finishes (one global atomic per block, see
+// ext_compact in nsd_kernels.hip): a global slot counter bumped per wave
+// serialises every wave of the chip on one word.
 struct ExtSink {
-	nsd_ext *ext;
-	uint32_t cap;
-	uint32_t *count;
+	nsd_ext *scr;        // this block's scratch entries (room for every packet it walks)
+	uint32_t *s_n;       // LDS: scratch entries taken
 };
 
 __device__ __forceinline__ uint16_t off_of(const WalkOut &w, uint32_t k)
@@ -96,46 +100,34 @@ __device__ __forceinline__ void record_layer(WalkOut &w, int id, const ExtSink &
 	} else {
 		w.need_ext = true;
 	}
-	// ext slot: one atomic per group of lanes reaching this point together
-	// (ballot / shfl / mbcnt over the active lanes), not one per lane
-	const bool want = w.need_ext && !w.ext_on && !(w.flags & NSD_F_OVERFLOW);
+	// scratch slot: one LDS atomic per group of lanes reaching this point
+	// together (ballot / shfl / mbcnt over the active lanes).  Only the used
+	// prefix of the entry is written (the layers past nlayers are undefined).
+	const bool want = w.need_ext && !w.ext_on;
 	const uint64_t wm = __ballot(want);
 	if (wm) {
 		const int leader = __ffsll((unsigned long long)wm) - 1;
 		uint32_t sb = 0;
 		if ((int)__lane_id() == leader)
-			sb = atomicAdd(es.count, (uint32_t)__popcll(wm));
+			sb = atomicAdd(es.s_n, (uint32_t)__popcll(wm));
 		sb = __shfl(sb, leader, 64);
 		sb += __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32),
 						__builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0));
 		if (want) {
-		const uint32_t s = sb;
-		if (s < es.cap) {
-			nsd_ext *e = es.ext + s;
-			uint32_t *z = (uint32_t *)e;   // entries past nlayers compare as zero
-			for (uint32_t j = 0; j < sizeof(nsd_ext) / 4; j++)
-				z[j] = 0;
-			uint32_t m = k < NSD_REC_MAX_LAYERS ? k : NSD_REC_MAX_LAYERS;
+			nsd_ext *e = es.scr + sb;
+			const uint32_t m = k < NSD_REC_MAX_LAYERS ? k : NSD_REC_MAX_LAYERS;
 			for (uint32_t j = 0; j < m; j++) {
 				e->id[j] = (uint8_t)((w.chain >> (5 * j)) & 31);
 				e->off[j] = off_of(w, j);
 			}
-			w.slot = s;
+			w.slot = sb;
 			w.ext_on = true;
-		} else {
-			w.flags |= NSD_F_OVERFLOW;
-			w.slot = 0xFFFFFFFFu;
-		}
 		}
 	}
 	if (w.ext_on) {
-#ifdef NSD_X_NOEXTW
-		if (0) {
-#else
 		if (k < NSD_EXT_MAX_LAYERS) {
-#endif
-			es.ext[w.slot].id[k] = (uint8_t)id;
-			es.ext[w.slot].off[k] = (uint16_t)w.data;
+			es.scr[w.slot].id[k] = (uint8_t)id;
+			es.scr[w.slot].off[k] = (uint16_t)w.data;
 		} else {
 			w.flags |= NSD_F_OVERFLOW;
 		}
