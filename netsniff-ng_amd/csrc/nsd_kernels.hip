@@ -34,8 +34,11 @@ constexpr int WAVES = BLOCK / 64;
 constexpr int WIN = 64;          // bytes per staged window
 constexpr int CPP = WIN / 16;    // 16-byte chunks per window
 constexpr int ROW = WIN / 4 + 1; // window row stride in dwords (odd: conflict-free reads)
-#ifndef NSD_DRAIN_G
-#define NSD_DRAIN_G 8              // pending checksums with loads in flight together per wave
+#ifndef NSD_CSUM_U
+#define NSD_CSUM_U 8               // interior chunk loads in flight per lane (dissect_icmp)
+#endif
+#ifndef NSD_CSUM_SPLIT
+#define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
 #endif
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
@@ -270,111 +273,11 @@ __device__ __forceinline__ uint32_t csum_chunk(const uint4 &v, uint32_t lo, uint
 	return sum_halves(v.w & msg_mask(lo + 12, s0, endb), acc);
 }
 
-// chunk j of a message: only chunk 0 and chunk nch - 1 can be partial, so
-// only their lanes take the masking path
-__device__ __forceinline__ uint32_t msg_chunk(const uint4 &v, uint32_t j, uint32_t s0, uint32_t endb,
-					      uint32_t nch, uint32_t acc)
-{
-	if (j == 0 || j == nch - 1)
-		return acc + csum_chunk(v, 16 * j, s0, endb);
-	acc = sum_halves(v.x, acc);
-	acc = sum_halves(v.y, acc);
-	acc = sum_halves(v.z, acc);
-	return sum_halves(v.w, acc);
-}
-
 __device__ __forceinline__ uint16_t csum_final(uint32_t sum)
 {
 	sum = (sum >> 16) + (sum & 0xffff);
 	sum += (sum >> 16);
 	return (uint16_t)~sum;
-}
-
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t v)
-{
-#pragma unroll
-	for (int o = 32; o > 0; o >>= 1)
-		v += __shfl_xor(v, o, 64);
-	return v;
-}
-
-// Checksums of the messages the walks left pending (past the staged
-// window), wave-cooperatively: G messages at a time, 64 lanes x 16 B = 1 KiB
-// per coalesced load and message, the G loads in flight together; the G
-// per-lane partial sums are reduced across the wave by a transposing
-// butterfly (G - 1 + log2(64 / G) shuffles instead of 6 G).  a = message
-// start in `frames`, nbytes even (odd byte dropped).
-template <int G>
-__device__ __forceinline__ void wave_icmp_csums(const uint8_t *frames, bool pend, uint64_t a,
-						 uint32_t nbytes, uint8_t &flags, int lane)
-{
-	static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "G must be a power of two <= 16");
-	uint64_t pm = __ballot(pend);
-	while (pm) {
-		int L[G];
-		uint32_t sum[G], s0[G], endb[G], nch[G];
-		const uint4 *p[G];
-		uint4 v[G];
-		// all G first-round loads issued before any is used
-#pragma unroll
-		for (int t = 0; t < G; t++) {
-			L[t] = pm ? __ffsll((unsigned long long)pm) - 1 : -1;
-			pm &= pm - 1;
-			nch[t] = 0;
-			if (L[t] >= 0) {
-				const uint32_t alo = __builtin_amdgcn_readlane((uint32_t)a, L[t]);
-				const uint32_t ahi = __builtin_amdgcn_readlane((uint32_t)(a >> 32), L[t]);
-				const uint32_t nb = __builtin_amdgcn_readlane(nbytes, L[t]);
-				s0[t] = alo & 15;
-				endb[t] = s0[t] + nb;
-				nch[t] = (endb[t] + 15) >> 4;
-				p[t] = (const uint4 *)(frames + ((((uint64_t)ahi << 32) | alo) & ~15ull));
-			}
-			v[t] = (uint32_t)lane < nch[t] ? p[t][lane] : make_uint4(0, 0, 0, 0);
-		}
-#pragma unroll
-		for (int t = 0; t < G; t++) {
-			sum[t] = 0;
-			if (L[t] >= 0) {
-				sum[t] = msg_chunk(v[t], lane, s0[t], endb[t], nch[t], 0u);
-				for (uint32_t j = lane + 64; j < nch[t]; j += 64)   // messages over 1 KiB
-					sum[t] = msg_chunk(p[t][j], j, s0[t], endb[t], nch[t], sum[t]);
-				sum[t] = (sum[t] >> 16) + (sum[t] & 0xffff);
-			}
-		}
-		// transposing butterfly: after the step at distance d, a lane keeps
-		// half of its sums, each added to its partner's matching one
-		int k = G;
-#pragma unroll
-		for (int d = 32; d >= 1; d >>= 1) {
-			if (k > 1) {
-				const bool hi = lane & d;
-				k >>= 1;
-#pragma unroll
-				for (int t = 0; t < k; t++) {
-					const uint32_t mine = hi ? sum[t + k] : sum[t];
-					const uint32_t give = hi ? sum[t] : sum[t + k];
-					sum[t] = mine + __shfl_xor(give, d, 64);
-				}
-			} else {
-				sum[0] += __shfl_xor(sum[0], d, 64);
-			}
-		}
-		// message t's total sits in the lanes whose distance bits spell t
-#pragma unroll
-		for (int t = 0; t < G; t++) {
-			if (L[t] < 0)
-				break;
-			int src = 0;
-#pragma unroll
-			for (int b = 0, d = 32; (1 << b) < G; b++, d >>= 1)
-				if (t & (G >> (b + 1)))
-					src |= d;
-			const uint32_t tot = __builtin_amdgcn_readlane(sum[0], src);
-			if (lane == L[t] && csum_final(tot))
-				flags |= NSD_F_ICMP_BAD;
-		}
-	}
 }
 
 // record words of a finished walk (layout of nsd_rec)
@@ -737,54 +640,80 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
 // Runs after both passes (the records are final): block b's waves take b's
-// lists, G messages' loads in flight per wave, and patch the flags byte of
-// the records whose sum is bad.
-constexpr uint32_t SMALL_CHUNKS = 6;
-
-template <int G>
+// lists in 64-entry pieces and patch the flags byte of the records whose sum
+// is bad.  Four lanes per message, 16 messages per wave at a time: lane
+// `sub` of a group sums the interior chunks 1 + sub + 4t (whole 16-byte
+// loads, no masking; each group instruction reads 64 contiguous bytes), U of
+// them in flight per lane; sub-lanes 0 and 1 also take the message's first
+// and last chunk with the bytes outside the message masked.  A message then
+// costs a few wave instructions per KiB instead of one wave per message.
+template <int U>
 __global__ __launch_bounds__(BLOCK) void dissect_icmp(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint4 *__restrict__ rec,
 	unsigned long long *__restrict__ counters, const uint64_t *__restrict__ pend,
-	const uint64_t *__restrict__ pend2, uint32_t region, const uint32_t *__restrict__ pcnt)
+	const uint64_t *__restrict__ pend2, uint32_t region, const uint32_t *__restrict__ pcnt,
+	uint32_t split)
 {
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
+	const uint32_t sub = lane & 3, grp = lane >> 2;
+	// `split` blocks share the lists of one pass-1 block
+	const uint32_t ob = blockIdx.x / split, part = blockIdx.x % split;
+	const uint32_t nw = WAVES * split, w0 = part * WAVES + wv;
 	uint32_t bad = 0;
 	for (int l = 0; l < PLISTS; l++) {
-		const uint32_t cnt = pcnt[blockIdx.x * PLISTS + l];
-		const uint64_t *list = l < WAVES ? pend + ((size_t)blockIdx.x * WAVES + l) * (region / WAVES)
-						 : pend2 + (size_t)blockIdx.x * region;
-		// the block's waves split each list in 64-entry pieces
-		for (uint32_t k0 = 64 * ((wv + l) % WAVES); k0 < cnt; k0 += 64 * WAVES) {
+		const uint32_t cnt = pcnt[ob * PLISTS + l];
+		const uint64_t *list = l < WAVES ? pend + ((size_t)ob * WAVES + l) * (region / WAVES)
+						 : pend2 + (size_t)ob * region;
+		// the waves of the `split` blocks split each list in 64-entry pieces
+		for (uint32_t k0 = 64 * ((w0 + l) % nw); k0 < cnt; k0 += 64 * nw) {
 			const bool on = k0 + lane < cnt;
 			const uint64_t e = on ? list[k0 + lane] : 0;
 			const uint32_t i = (uint32_t)e;
 			const uint32_t moff = (uint32_t)(e >> 32) & 0xFFFF, mlen = (uint32_t)(e >> 48);
 			const uint64_t a = (on ? NSD_DESC_OFF(desc[i]) : 0) + moff;
-			const uint32_t nb = mlen & ~1u;
-			// short messages (the 64 B frames of a mix): one lane each;
-			// longer ones: the whole wave per message
-			const bool small = on && (a & 15) + nb <= 16 * SMALL_CHUNKS;
-			uint8_t fl = 0;
-			if (__ballot(small)) {
-				if (small) {
-					const uint4 *p = (const uint4 *)(frames + (a & ~15ull));
-					const uint32_t s0 = (uint32_t)(a & 15), endb = s0 + nb;
-					uint32_t sum = 0;
+			const uint32_t nb = on ? (mlen & ~1u) : 0u;
+			for (uint32_t q = 0; q < 64 && k0 + q < cnt; q += 16) {
+				const int src = (int)(q + grp);
+				const uint32_t alo = __shfl((uint32_t)a, src, 64);
+				const uint32_t ahi = __shfl((uint32_t)(a >> 32), src, 64);
+				const uint32_t mnb = __shfl(nb, src, 64);
+				const bool mon = k0 + (uint32_t)src < cnt;
+				const uint32_t s0 = alo & 15, endb = s0 + mnb;
+				const uint32_t nch = mon ? (endb + 15) >> 4 : 0u;
+				const uint4 *base = (const uint4 *)(frames + ((((uint64_t)ahi << 32) | alo) & ~15ull));
+				// edge chunks, masked: chunk 0 on sub-lane 0, chunk nch-1 on sub-lane 1
+				uint32_t sum = 0;
+				const uint32_t je = sub == 0 ? 0u : nch - 1;
+				if ((sub == 0 && nch > 0) || (sub == 1 && nch > 1))
+					sum = csum_chunk(base[je], 16 * je, s0, endb);
+				// interior chunks [1, nch - 1)
+				for (uint32_t j = 1 + sub; __ballot(j + 1 < nch); j += 4 * U) {
+					uint4 v[U];
 #pragma unroll
-					for (uint32_t j = 0; j < SMALL_CHUNKS; j++)
-						if (16 * j < endb)
-							sum += csum_chunk(p[j], 16 * j, s0, endb);
-					if (csum_final(sum))
-						fl = NSD_F_ICMP_BAD;
+					for (int u = 0; u < U; u++) {
+						const uint32_t jj = j + 4 * u;
+						v[u] = jj + 1 < nch ? base[jj] : make_uint4(0, 0, 0, 0);
+					}
+#pragma unroll
+					for (int u = 0; u < U; u++) {
+						sum = sum_halves(v[u].x, sum);
+						sum = sum_halves(v[u].y, sum);
+						sum = sum_halves(v[u].z, sum);
+						sum = sum_halves(v[u].w, sum);
+					}
 				}
+				sum = (sum >> 16) + (sum & 0xffff);   // folding keeps the zero test
+				sum += __shfl_xor(sum, 1, 64);
+				sum += __shfl_xor(sum, 2, 64);
+				const uint32_t mi = __shfl(i, src, 64);
+				const bool isbad = mon && sub == 0 && csum_final(sum) != 0;
+				if (isbad) {
+					uint8_t *nf = (uint8_t *)rec + (size_t)mi * 16 + 10;
+					*nf = *nf | NSD_F_ICMP_BAD;
+				}
+				bad += FlagCnt::pc(isbad);
 			}
-			wave_icmp_csums<G>(frames, on && !small, a, nb, fl, lane);
-			if (fl) {
-				uint8_t *nf = (uint8_t *)rec + (size_t)i * 16 + 10;
-				*nf = *nf | NSD_F_ICMP_BAD;
-			}
-			bad += FlagCnt::pc(fl != 0);
 		}
 	}
 	if (lane == 0 && bad)
@@ -872,8 +801,8 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 		hipLaunchKernelGGL(dissect_general<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
 				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
 				   region, qblk, pend2, pcnt, scratch);
-		hipLaunchKernelGGL(dissect_icmp<NSD_DRAIN_G>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, rec, cnt, pend, pend2, region, pcnt);
+		hipLaunchKernelGGL(dissect_icmp<NSD_CSUM_U>, dim3(blocks * NSD_CSUM_SPLIT), dim3(BLOCK), 0, stream,
+				   d_frames, d_desc, rec, cnt, pend, pend2, region, pcnt, (uint32_t)NSD_CSUM_SPLIT);
 		break;
 	case PRINT_LESS:
 		hipLaunchKernelGGL(dissect_fast<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,

@@ -146,3 +146,28 @@ def test_pipe_batches(depth):
         assert np.array_equal(cnt, ocnt)
     assert pipe.wait() == 1
     pipe.close()
+
+
+def _icmp_sweep(seed=7):
+    """ICMPv4 messages of every length class the checksum paths split on
+    (inside the staged window, just past it, 1-2 KiB, > 2 KiB), good and
+    bad sums, odd lengths, VLAN-shifted and IPv4-trimmed (trailer) frames."""
+    import random
+    rnd = random.Random(seed)
+    E = edge_cases
+    pkts = []
+    for plen in list(range(0, 80)) + list(range(80, 3000, 37)) + [4000, 8000, 9000]:
+        body = bytes(rnd.randrange(256) for _ in range(plen))
+        for good in (True, False):
+            for vlan in (False, True):
+                l2 = E.eth(0x8100) + E.be16(5) + E.be16(0x0800) if vlan else E.eth(0x0800)
+                msg = E.icmp(payload=body, good=good)
+                trailer = bytes(rnd.randrange(256) for _ in range(rnd.choice([0, 0, 3, 17])))
+                pkts.append(l2 + E.ipv4(1, len(msg)) + msg + trailer)
+    return pkts
+
+
+@pytest.mark.parametrize("align", [1, 2, 16])
+def test_icmp_checksum_sweep(align):
+    frames, desc = T.batch_from_packets(_icmp_sweep(), align=align)
+    _check(frames, desc, T.PRINT_NORM)
