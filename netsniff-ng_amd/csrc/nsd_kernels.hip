@@ -62,6 +62,7 @@ template <bool FAST>
 struct LSrc {
 	const uint32_t *win;     // this lane's window row
 	const uint8_t *lay3t;    // LDS copy of eth_lay3
+	const uint32_t *stept;   // LDS copy of c_step, then c_lay2h (general walk)
 	const uint8_t *p;        // frame in HBM
 	uint32_t caplen;
 	uint32_t m;              // off & 15
@@ -70,6 +71,19 @@ struct LSrc {
 
 	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return win[j]; }
 	__device__ __forceinline__ int lay3(uint32_t key) const { return lay3t[key & 255]; }
+	__device__ __forceinline__ uint32_t step(int id) const { return stept[id & 31]; }
+	__device__ __forceinline__ uint32_t l2h(uint32_t h) const { return stept[32 + (h & 31)]; }
+	// bytes o .. o+3 (little-endian) from the window row: two dwords and a
+	// byte funnel shift; zero at offsets >= caplen.  Meaningful only for
+	// bytes inside the window (a near_end() budget covers them).
+	__device__ __forceinline__ uint32_t dword_at(uint32_t o) const
+	{
+		const uint32_t r = o + m - wb;
+		uint32_t j = r >> 2;
+		j = j > 15 ? 15 : j;
+		const uint32_t v = __builtin_amdgcn_alignbyte(dw(j + 1), dw(j), r & 3);
+		return o >= caplen ? 0u : v;
+	}
 	__device__ __forceinline__ bool missed() const { return miss; }
 	__device__ __forceinline__ uint8_t b(uint32_t o) const
 	{
@@ -95,27 +109,34 @@ struct LSrc {
 	{
 		return (uint16_t)__builtin_bswap16(le16(o));
 	}
+	// bytes o .. o+15 as four little-endian dwords (5 window dwords + byte
+	// funnel shifts).  Only the bytes the caller's near_end() budget covers
+	// are meaningful (later ones may come from the next window row); bytes
+	// at offsets >= caplen are zero.
+	__device__ __forceinline__ void bytes16(uint32_t o, uint32_t &B0, uint32_t &B1, uint32_t &B2,
+						uint32_t &B3) const
+	{
+		const uint32_t r = o + m - wb;
+		uint32_t j = r >> 2;
+		j = j > 15 ? 15 : j;
+		const uint32_t sh = r & 3;
+		const uint32_t w0 = dw(j), w1 = dw(j + 1), w2 = dw(j + 2), w3 = dw(j + 3), w4 = dw(j + 4);
+		const bool z = o >= caplen;
+		B0 = z ? 0u : __builtin_amdgcn_alignbyte(w1, w0, sh);
+		B1 = z ? 0u : __builtin_amdgcn_alignbyte(w2, w1, sh);
+		B2 = z ? 0u : __builtin_amdgcn_alignbyte(w3, w2, sh);
+		B3 = z ? 0u : __builtin_amdgcn_alignbyte(w4, w3, sh);
+	}
 	__device__ __forceinline__ bool in_window(uint32_t o, uint32_t nbytes) const
 	{
 		const uint32_t r = o + m - wb;
 		return r < WIN && r + nbytes <= WIN;
 	}
-	// the next layer would read past the staged window (bytes its process()
-	// inspects, from its start; longer reads such as IPv4 options use the
-	// fallback)
+	// the next layer would read past the staged window (the bytes its parse
+	// inspects from its start, c_step's `need`): general walk only
 	__device__ __forceinline__ bool near_end(uint32_t o, int id) const
 	{
-		uint32_t need;
-		switch (id) {
-		case NSD_OPS_ETHERNET: need = 14; break;
-		case NSD_OPS_IPV4: need = 20; break;
-		case NSD_OPS_MPLS_UC: need = 16; break;
-		case NSD_OPS_IPV6: case NSD_OPS_IPV6_IN_IPV4: need = 8; break;
-		case NSD_OPS_VLAN: case NSD_OPS_QINQ: case NSD_OPS_IPV6_HOP_BY_HOP:
-		case NSD_OPS_IPV6_DEST_OPTS: case NSD_OPS_IPV6_ROUTING: case NSD_OPS_IPV6_FRAGM:
-		case NSD_OPS_IP_AUTH: case NSD_OPS_IPV6_MOBILITY: case NSD_OPS_ICMPV6: need = 4; break;
-		default: need = 0;
-		}
+		const uint32_t need = step(id) >> 24;
 		return need && o < caplen && o + m + need > wb + WIN;
 	}
 	// sum of `nwords` little-endian u16 words from `o` (csum.h:16-17)
@@ -133,28 +154,6 @@ struct LSrc {
 		for (uint32_t i = 0; i < nwords; i++)
 			sum += le16(o + 2 * i);
 		return sum;
-	}
-};
-
-// Wave-aggregated per-layer counting into the block's LDS counters (pass 2):
-// active lanes are grouped by ops id, the group leader adds its size.
-struct WaveCnt {
-	unsigned long long *s_cnt;
-	__device__ __forceinline__ void operator()(int id) const
-	{
-		int my = id;
-		for (;;) {
-			const uint64_t pend = __ballot(my >= 0);
-			if (!pend)
-				break;
-			const int leader = __ffsll((unsigned long long)pend) - 1;
-			const int lid = __shfl(my, leader, 64);
-			const uint64_t m = __ballot(my == lid);
-			if ((int)__lane_id() == leader)
-				atomicAdd(&s_cnt[NSD_CNT_OPS + lid], (unsigned long long)__popcll(m));
-			if (my == lid)
-				my = -1;
-		}
 	}
 };
 
@@ -435,7 +434,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		walk_init(w, caplen, valid ? start_id : 0);
 		bool deferred = false;
 		if (valid) {
-			const LSrc<true> src{ &s_win[wv][lane * ROW], s_lay3, frames + off, caplen,
+			const LSrc<true> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
 					      (uint32_t)off & 15, 0, false };
 #ifdef NSD_X_NOWALK
 			w.chain = src.dw(3) & 0x3FF; w.n = 2; w.data = 42;
@@ -504,9 +503,10 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 // table at a range taken with one global atomic (so the table stays compact:
 // entries [0, min(count, cap)) are filled), and each owner record gets its
 // final slot (bytes 10..15: nflags, slot).  Entries past the capacity leave
-// their record with NSD_F_OVERFLOW and slot 0xFFFFFFFF.  Only the used
-// dwords of an entry are copied, 16 lanes per entry.
-__device__ __forceinline__ void ext_compact(const nsd_ext *scr, uint32_t &s_en, uint32_t &s_ebase,
+// their record with NSD_F_OVERFLOW and slot 0xFFFFFFFF.  16 lanes per entry,
+// lane t converting layers 4t .. 4t+3 (packed u32 -> id bytes + offsets);
+// entries past nlayers are not written.
+__device__ __forceinline__ void ext_compact(const ExtScr *scr, uint32_t &s_en, uint32_t &s_ebase,
 					    uint4 *rec, nsd_ext *ext, uint32_t ext_cap,
 					    uint32_t *ext_count, unsigned long long *counters)
 {
@@ -518,23 +518,38 @@ __device__ __forceinline__ void ext_compact(const nsd_ext *scr, uint32_t &s_en, 
 	const uint32_t t = threadIdx.x & 15;
 	uint32_t ovf = 0;
 	for (uint32_t j = threadIdx.x >> 4; j < ne; j += BLOCK / 16) {
-		const uint32_t *src = (const uint32_t *)(scr + j);
-		const uint32_t h1 = src[1];
-		const uint32_t nl = h1 & 0xFFFF, nf = h1 >> 16;
+		const ExtScr *src = scr + j;
+		const uint32_t pkt = src->pkt, hdr = src->hdr;
+		const uint32_t nl = hdr & 0xFFFF, nf = hdr >> 16;
 		const uint32_t slot = base + j;
 		const bool fits = slot < ext_cap;
 		if (fits) {
-			uint32_t *dst = (uint32_t *)(ext + slot);
-			const uint32_t idw = 2 + (nl + 3) / 4, offw = 18 + (nl + 1) / 2;
-			for (uint32_t x = t; x < sizeof(nsd_ext) / 4; x += 16) {
-				if (x < idw || (x >= 18 && x < offw))
-					dst[x] = x == 1 ? nl : src[x];
+			uint8_t *dst = (uint8_t *)(ext + slot);
+			if (t == 0) {
+				*(uint32_t *)dst = pkt;
+				*(uint32_t *)(dst + 4) = nl;   // nlayers, rsvd 0
+			}
+			if (4 * t < nl) {
+				const uint4 l = *(const uint4 *)&src->lay[4 * t];
+				const uint32_t x[4] = { l.x, l.y, l.z, l.w };
+				uint32_t ids = 0, o01 = 0, o23 = 0;
+#pragma unroll
+				for (uint32_t u = 0; u < 4; u++) {
+					const uint32_t v = 4 * t + u < nl ? x[u] : 0u;
+					ids |= (v & 0xFF) << (8 * u);
+					if (u < 2)
+						o01 |= (v >> 16) << (16 * u);
+					else
+						o23 |= (v >> 16) << (16 * (u - 2));
+				}
+				*(uint32_t *)(dst + offsetof(nsd_ext, id) + 4 * t) = ids;
+				*(uint2 *)(dst + offsetof(nsd_ext, off) + 8 * t) = make_uint2(o01, o23);
 			}
 		}
 		if (t == 0) {
 			const uint32_t s = fits ? slot : 0xFFFFFFFFu;
 			const uint32_t f = fits ? nf : nf | NSD_F_OVERFLOW;
-			uint8_t *r = (uint8_t *)(rec + src[0]);
+			uint8_t *r = (uint8_t *)(rec + pkt);
 			*(uint16_t *)(r + 10) = (uint16_t)((f & 0xFF) | (s & 0xFF) << 8);
 			*(uint32_t *)(r + 12) = s >> 8;
 			ovf += !fits && !(nf & NSD_F_OVERFLOW);
@@ -551,12 +566,13 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	uint4 *__restrict__ rec, nsd_ext *__restrict__ ext, uint32_t ext_cap,
 	uint32_t *__restrict__ ext_count, unsigned long long *__restrict__ counters,
 	const uint32_t *__restrict__ queue, uint32_t region, const uint32_t *__restrict__ qblk,
-	uint64_t *__restrict__ pend2, uint32_t *__restrict__ pcnt, nsd_ext *__restrict__ scratch)
+	uint64_t *__restrict__ pend2, uint32_t *__restrict__ pcnt, ExtScr *__restrict__ scratch)
 {
 	__shared__ uint32_t s_win[WAVES][64 * ROW];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
 	__shared__ uint8_t s_lay3[256];
 	__shared__ uint32_t s_pn, s_en, s_ebase;
+	__shared__ uint32_t s_step[64];   // c_step, c_lay2h
 
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
@@ -564,15 +580,17 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 		s_pn = 0;
 		s_en = 0;
 	}
+	if (threadIdx.x < 64)
+		s_step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h[threadIdx.x - 32];
+	// (block_init's barrier orders these)
 	block_init(s_cnt, s_lay3);
 	uint64_t *const bp = pend2 + (size_t)blockIdx.x * region;   // this block's pending list
 
 	// block b drains the queue region pass 1's block b filled
 	const uint32_t nq = qblk[blockIdx.x];
 	const uint32_t *const bq = queue + (size_t)blockIdx.x * region;
-	const WaveCnt wc{ s_cnt };
-	nsd_ext *const scr = scratch + (size_t)blockIdx.x * region;   // this block's ext scratch
-	const ExtSink es{ scr, &s_en };
+	ExtScr *const scr = scratch + (size_t)blockIdx.x * region;   // this block's ext scratch
+	const GenSink g{ scr, &s_en, s_cnt };
 	FlagCnt fc;
 
 	for (uint32_t base = wv * 64; base < nq; base += BLOCK) {
@@ -596,10 +614,18 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 			stage_load<true>(ch, frames, d, wbp, lane);
 			stage_write(&s_win[wv][0], ch, lane);
 			wave_sync_lds();
-			bool susp = false;
-			if (part) {
-				const LSrc<false> src{ &s_win[wv][lane * ROW], s_lay3, frames + off, caplen, m, wb, false };
-				susp = walk<MODE, false>(src, caplen, es, w, wc);
+			const LSrc<false> src{ &s_win[wv][lane * ROW], s_lay3, s_step, frames + off, caplen, m, wb,
+					       false };
+			bool susp;
+			for (;;) {
+				// a lane whose next layer would read past its window
+				// suspends for the rest of this round
+				const bool run = part && w.id != 0;
+				susp = run && src.near_end(w.data, w.id);
+				const bool act = run && !susp;
+				if (!__ballot(act))
+					break;
+				gen_step<MODE>(src, act, w, g);
 			}
 			wave_sync_lds();
 			if (!__ballot(susp))
@@ -623,10 +649,10 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 		if (!valid)
 			continue;
 		if (w.ext_on) {
-			nsd_ext *e = scr + w.slot;
+			ExtScr *e = scr + w.slot;
 			e->pkt = i;
-			e->nlayers = (uint16_t)(w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS);
-			e->rsvd = (uint16_t)(NSD_N_EXT | w.flags);   // the record's nflags, for ext_compact
+			e->hdr = (w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS) |
+				 (uint32_t)(NSD_N_EXT | w.flags) << 16;   // the record's nflags, for ext_compact
 		}
 		rec[i] = pack_record(w);
 		fc.add(w, caplen, true);
@@ -743,10 +769,10 @@ static size_t region_slots(uint32_t n)
 
 // workspace: qblk[NSD_MAX_GRID], pcnt[NSD_MAX_GRID * 8], the deferral queue
 // (u32 per slot), the pass-1 and pass-2 pending-checksum lists (u64 per slot),
-// pass 2's per-block ext scratch (nsd_ext per slot, 8-byte aligned)
+// pass 2's per-block ext scratch (ExtScr per slot, 16-byte aligned)
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
-	return 4 * (size_t)NSD_MAX_GRID * 9 + (4 + 8 + 8 + sizeof(nsd_ext)) * region_slots(n);
+	return 4 * (size_t)NSD_MAX_GRID * 9 + 16 + (4 + 8 + 8 + sizeof(nsd::ExtScr)) * region_slots(n);
 }
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
@@ -793,7 +819,7 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	uint32_t *queue = pcnt + 8 * NSD_MAX_GRID;
 	uint64_t *pend = (uint64_t *)(queue + region_slots(n));
 	uint64_t *pend2 = pend + region_slots(n);
-	nsd_ext *scratch = (nsd_ext *)(pend2 + region_slots(n));
+	ExtScr *scratch = (ExtScr *)(((uintptr_t)(pend2 + region_slots(n)) + 15) & ~(uintptr_t)15);
 	switch (mode) {
 	case PRINT_NORM:
 		hipLaunchKernelGGL(dissect_fast<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,

@@ -69,70 +69,26 @@ struct WalkOut {
 	uint32_t icmp_off, icmp_len;
 };
 
-// Ext spill: the first time a packet needs the ext form it takes a slot in
-// its block's scratch table (LDS counter, one add per group of lanes reaching
-// that point together) and copies the layers collected so far; later layers
-// go straight to the slot.  The block compacts its scratch entries into the
-// caller's ext table when it finishes (one global atomic per block, see
-// ext_compact in nsd_kernels.hip): a global slot counter bumped per wave
-// serialises every wave of the chip on one word.
-struct ExtSink {
-	nsd_ext *scr;        // this block's scratch entries (room for every packet it walks)
-	uint32_t *s_n;       // LDS: scratch entries taken
+// Pass 2's ext scratch entry (block-local, see ext_compact in
+// nsd_kernels.hip): one packed u32 per layer (ops id | start offset << 16),
+// so recording a layer is one store.
+struct ExtScr {
+	uint32_t pkt;
+	uint32_t hdr;                        // nlayers | record nflags << 16
+	uint32_t pad[2];                     // lay[] 16-byte aligned (ext_compact reads uint4)
+	uint32_t lay[NSD_EXT_MAX_LAYERS];
+};
+
+// Where the general walk puts what it records beyond the 16-byte record.
+struct GenSink {
+	ExtScr *scr;                  // this block's scratch entries (room for every packet it walks)
+	uint32_t *s_n;                // LDS: scratch entries taken
+	unsigned long long *s_cnt;    // LDS: block counters
 };
 
 __device__ __forceinline__ uint16_t off_of(const WalkOut &w, uint32_t k)
 {
 	return k < 4 ? (uint16_t)(w.offA >> (16 * k)) : (uint16_t)(w.offB >> (16 * (k - 4)));
-}
-
-__device__ __forceinline__ void record_layer(WalkOut &w, int id, const ExtSink &es)
-{
-	const uint32_t k = w.n;
-	if (k < NSD_REC_MAX_LAYERS) {
-		w.chain |= (uint32_t)id << (5 * k);
-		if (k < 4)
-			w.offA |= (uint64_t)(w.data & 0xFFFF) << (16 * k);
-		else
-			w.offB |= (w.data & 0xFFFF) << (16 * (k - 4));
-		if (k >= 1 && w.data > 510)
-			w.need_ext = true;
-	} else {
-		w.need_ext = true;
-	}
-	// scratch slot: one LDS atomic per group of lanes reaching this point
-	// together (ballot / shfl / mbcnt over the active lanes).  Only the used
-	// prefix of the entry is written (the layers past nlayers are undefined).
-	const bool want = w.need_ext && !w.ext_on;
-	const uint64_t wm = __ballot(want);
-	if (wm) {
-		const int leader = __ffsll((unsigned long long)wm) - 1;
-		uint32_t sb = 0;
-		if ((int)__lane_id() == leader)
-			sb = atomicAdd(es.s_n, (uint32_t)__popcll(wm));
-		sb = __shfl(sb, leader, 64);
-		sb += __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32),
-						__builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0));
-		if (want) {
-			nsd_ext *e = es.scr + sb;
-			const uint32_t m = k < NSD_REC_MAX_LAYERS ? k : NSD_REC_MAX_LAYERS;
-			for (uint32_t j = 0; j < m; j++) {
-				e->id[j] = (uint8_t)((w.chain >> (5 * j)) & 31);
-				e->off[j] = off_of(w, j);
-			}
-			w.slot = sb;
-			w.ext_on = true;
-		}
-	}
-	if (w.ext_on) {
-		if (k < NSD_EXT_MAX_LAYERS) {
-			es.scr[w.slot].id[k] = (uint8_t)id;
-			es.scr[w.slot].off[k] = (uint16_t)w.data;
-		} else {
-			w.flags |= NSD_F_OVERFLOW;
-		}
-	}
-	w.n = k + 1;
 }
 
 // csum() (csum.h:12-22) over `nwords` little-endian u16 words from `off`
@@ -165,241 +121,231 @@ __device__ __forceinline__ void walk_init(WalkOut &w, uint32_t caplen, int start
 	w.icmp_len = 0;
 }
 
-// The walk (dissector_main's loop, dissector.c:51-58).  MODE is PRINT_NORM
-// or PRINT_LESS (parse semantics differ).  Runs layers until the chain ends
-// or, when `resumable`, until the next layer starts too close to the end of
-// the source's staged window (returns true: restage at w.data and call again).
-// Cnt: per-ops counter hook cnt(id).
-//
-// FAST (the first-pass kernel): instead of suspending, spilling to the ext
-// table or deferring an ICMP checksum, the walk gives up (returns true) and
-// the packet is queued for the general kernel, which walks it from scratch;
-// counting is left to the caller (from the finished record).
-template <int MODE, bool FAST, class Src, class Cnt>
-__device__ __forceinline__ bool walk(const Src &s, uint32_t caplen, const ExtSink &es, WalkOut &w,
-				     Cnt &&cnt)
+// Per-ops step table for the general walk: the first pull (minl), the fixed
+// advance, the rule kind, the byte offset of the next-ops key (kpos; a
+// big-endian u16 ethertype looked up in eth_lay2 when kw16, else a u8 looked
+// up in eth_lay3) and `need`, the bytes from the layer start its parse
+// reads (a lane whose window ends earlier suspends and is restaged; longer
+// reads such as IPv4 options or deep MPLS stacks use the byte source's
+// global fallback).  Per-ops semantics are cited in gen_step.
+enum : uint32_t {
+	K_HOST = 0,   // host-rendered leaf: ARP, LLDP, IGMP, DCCP, non-Ethernet heads
+	K_CONT = 1,   // fixed pull, continue with the key's ops
+	K_LEAF = 2,   // fixed pull, chain ends
+	K_IPV4 = 3,
+	K_T8 = 4,     // HBH / DestOpts / Routing: (hdr_ext_len + 1) * 8
+	K_AH = 5,
+	K_MOB = 6,
+	K_ICMP6 = 7,
+	K_MPLS = 8,
+};
+#define NSD_STEP(minl, adv, kind, kpos, kw16, need) \
+	((minl) | (adv) << 8 | (kind) << 16 | (kpos) << 20 | (kw16) << 24 | (uint32_t)(need) << 25)
+__constant__ uint32_t c_step[32] = {
+	/*  0 invalid   */ NSD_STEP(0, 0, K_HOST, 0, 0, 0),
+	/*  1 ethernet  */ NSD_STEP(14, 14, K_CONT, 12, 1, 14),   // proto_ethernet.c:48-79
+	/*  2 vlan      */ NSD_STEP(4, 4, K_CONT, 2, 1, 4),       // proto_vlan.c:22-40
+	/*  3 qinq      */ NSD_STEP(4, 4, K_CONT, 2, 1, 4),       // proto_vlan_q_in_q.c:23-41
+	/*  4 mpls      */ NSD_STEP(0, 0, K_MPLS, 0, 0, 16),      // proto_mpls_unicast.c:49-77
+	/*  5 arp       */ NSD_STEP(0, 0, K_HOST, 0, 0, 0),
+	/*  6 lldp      */ NSD_STEP(0, 0, K_HOST, 0, 0, 0),
+	/*  7 ipv4      */ NSD_STEP(20, 20, K_IPV4, 9, 0, 20),    // proto_ipv4.c:34-178
+	/*  8 ipv6      */ NSD_STEP(40, 40, K_CONT, 6, 0, 8),     // proto_ipv6.c:22-105
+	/*  9 ipv6inv4  */ NSD_STEP(40, 40, K_CONT, 6, 0, 8),     // proto_ipv6_in_ipv4.c:20-24
+	/* 10 icmpv4    */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0),       // proto_icmpv4.c:34-51
+	/* 11 icmpv6    */ NSD_STEP(4, 4, K_ICMP6, 0, 0, 4),      // proto_icmpv6.c:1667-1699
+	/* 12 igmp      */ NSD_STEP(0, 0, K_HOST, 0, 0, 0),
+	/* 13 ah        */ NSD_STEP(12, 12, K_AH, 0, 0, 4),       // proto_ip_authentication_hdr.c:26-69
+	/* 14 esp       */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0),       // proto_ip_esp.c:23-35
+	/* 15 destopts  */ NSD_STEP(2, 2, K_T8, 0, 0, 4),         // proto_ipv6_dest_opts.c:40-72
+	/* 16 fragm     */ NSD_STEP(8, 8, K_CONT, 0, 0, 4),       // proto_ipv6_fragm.c:25-47
+	/* 17 hopbyhop  */ NSD_STEP(2, 2, K_T8, 0, 0, 4),         // proto_ipv6_hop_by_hop.c:39-71
+	/* 18 mobility  */ NSD_STEP(6, 6, K_MOB, 0, 0, 4),        // proto_ipv6_mobility_hdr.c:247-309
+	/* 19 nonext    */ NSD_STEP(0, 0, K_LEAF, 0, 0, 0),       // proto_ipv6_no_nxt_hdr.c:17-29
+	/* 20 routing   */ NSD_STEP(4, 4, K_T8, 0, 0, 4),         // proto_ipv6_routing.c:79-122
+	/* 21 tcp       */ NSD_STEP(20, 20, K_LEAF, 0, 0, 0),     // proto_tcp.c:63-107 (options not pulled)
+	/* 22 udp       */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0),       // proto_udp.c:23-58
+	/* 23..31: dccp, none, sll, 802.11, nlmsg, unused: host leaves */
+};
+
+// eth_lay2 (dissector_eth.c:30-39) as a 32-entry perfect hash for the
+// general walk: slot ((key * 0x156) & 0xFFFF) >> 11 holds key | ops << 16
+// (one LDS read + compare instead of a 7-way compare tree)
+#define NSD_L2H(key) ((((key) * 0x156u) & 0xFFFFu) >> 11)
+__constant__ uint32_t c_lay2h[32] = {
+	[NSD_L2H(0x0806)] = 0x0806 | NSD_OPS_ARP << 16,
+	[NSD_L2H(0x88cc)] = 0x88cc | NSD_OPS_LLDP << 16,
+	[NSD_L2H(0x8100)] = 0x8100 | NSD_OPS_VLAN << 16,
+	[NSD_L2H(0x0800)] = 0x0800 | NSD_OPS_IPV4 << 16,
+	[NSD_L2H(0x86DD)] = 0x86DD | NSD_OPS_IPV6 << 16,
+	[NSD_L2H(0x88a8)] = 0x88a8 | NSD_OPS_QINQ << 16,
+	[NSD_L2H(0x8847)] = 0x8847 | NSD_OPS_MPLS_UC << 16,
+};
+
+// get_mh_type's subtype pull sizes for mobility types 0..7
+// (proto_ipv6_mobility_hdr.c:206-245), one byte per type
+#define NSD_MH_SUB 0x0A060612120A0A02ull
+
+// The general walk (pass 2), one layer per call for every lane of the wave:
+// dissector_main's loop body (dissector.c:51-58) for the ops `w.id`,
+// computed as straight-line selects over a per-ops rule table rather than a
+// switch, so a wave whose lanes sit at different layers runs one instruction
+// stream (a divergent switch runs every case body present plus its exec-mask
+// bookkeeping, which made the scalar unit the bottleneck).  The rare heavy
+// bodies (IPv4 header checksum, ICMPv4 checksum, MPLS label walk) sit behind
+// wave-uniform branches.  `act`: the lane runs a layer in this call.  Per
+// layer: record the ops (chain word / offsets, or the ext scratch entry once
+// the chain needs the ext form), count it, advance the pkt_buff cursor
+// exactly as the reference parser does, look up the next ops.
+template <int MODE, class Src>
+__device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, const GenSink &g)
 {
-	(void)caplen;
-	while (w.id) {
-		const int id = w.id;
-		if (s.near_end(w.data, id))
-			return true;
-		if constexpr (FAST) {
-			if (w.n >= NSD_REC_MAX_LAYERS || (w.n >= 1 && w.data > 510))
-				return true;
-			w.chain |= (uint32_t)id << (5 * w.n);
-			if (w.n < 4)
-				w.offA |= (uint64_t)w.data << (16 * w.n);
-			else
-				w.offB |= w.data << (16 * (w.n - 4));
-			w.n++;
-		} else {
-			record_layer(w, id, es);
-			cnt(w.n <= NSD_EXT_MAX_LAYERS ? id : -1);   // the oracle counts the first 64 layers
+	const int id = act ? w.id : 0;
+	const uint32_t start = w.data;
+	const uint32_t k = w.n;
+	// ---- record the layer: the first 6 in the record; more than 6, or a
+	// layer past byte 510, forces the ext form
+	const bool need_now = act && (k >= NSD_REC_MAX_LAYERS || (k >= 1 && start > 510));
+	const bool first = need_now && !w.ext_on;
+	const uint64_t fm = __ballot(first);
+	if (fm) {
+		const int leader = __ffsll((unsigned long long)fm) - 1;
+		uint32_t sb = 0;
+		if ((int)__lane_id() == leader)
+			sb = atomicAdd(g.s_n, (uint32_t)__popcll(fm));
+		sb = __shfl(sb, leader, 64);
+		sb += __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0));
+		if (first) {
+			ExtScr *e = g.scr + sb;
+#pragma unroll
+			for (uint32_t j = 0; j < NSD_REC_MAX_LAYERS; j++)
+				if (j < k)
+					e->lay[j] = ((w.chain >> (5 * j)) & 31) | (uint32_t)off_of(w, j) << 16;
+			w.slot = sb;
+			w.ext_on = true;
 		}
-		const uint32_t start = w.data;
-		const uint32_t len = w.tail - w.data;   // pkt_len (pkt_buff.h:36-41)
-		int next = 0;
-		switch (id) {
-		case NSD_OPS_ETHERNET:      // proto_ethernet.c:48-79
-			if (len >= 14) {
-				next = lay2(s.be16(start + 12));
-				w.data = start + 14;
+	}
+	const uint32_t kk = k < 8 ? k : 7;   // keeps the shifts below defined
+	w.need_ext = w.need_ext || need_now;
+	w.chain |= act && k < NSD_REC_MAX_LAYERS ? (uint32_t)id << (5 * kk) : 0u;
+	w.offA |= act && k < 4 ? (uint64_t)(start & 0xFFFF) << (16 * (kk & 3)) : 0ull;
+	w.offB |= act && k >= 4 && k < NSD_REC_MAX_LAYERS ? (start & 0xFFFF) << (16 * (kk & 1)) : 0u;
+	w.flags |= act && k >= NSD_EXT_MAX_LAYERS && w.ext_on ? NSD_F_OVERFLOW : 0;
+	if (act && k < NSD_EXT_MAX_LAYERS) {
+		atomicAdd(&g.s_cnt[NSD_CNT_OPS + id], 1ull);   // the oracle counts the first 64 layers
+		if (w.ext_on)
+			g.scr[w.slot].lay[k] = (uint32_t)id | start << 16;
+	}
+	w.n = act ? k + 1 : k;
+
+	// ---- parse (bytes >= caplen read as zero).  Everything below is
+	// computed for every lane and selected by the rule kind; boolean terms
+	// are combined with & and | so the compiler keeps them as selects.
+	const uint32_t len = w.tail - start;   // pkt_len (pkt_buff.h:36-41)
+	const uint32_t info = s.step(id);
+	const uint32_t minl = info & 0xFF, fadv = (info >> 8) & 0xFF, kind = (info >> 16) & 0xF,
+		       kpos = (info >> 20) & 0xF;
+	const bool kw16 = (info >> 24) & 1;
+	const uint32_t B0 = s.dword_at(start);          // layer bytes 0..3
+	const uint32_t KD = s.dword_at(start + kpos);   // the next-ops key's bytes
+	const uint32_t b0 = B0 & 0xFF, b1 = (B0 >> 8) & 0xFF, b2 = (B0 >> 16) & 0xFF;
+	const uint32_t k2 = __builtin_bswap16((uint16_t)(B0 >> 16));   // IPv4 tot_len
+	const uint32_t key16 = __builtin_bswap16((uint16_t)KD);
+	const uint32_t e2 = s.l2h(NSD_L2H(key16));
+	// eth_lay2 / eth_lay3 (dissector_eth.c:30-62)
+	const int nx = kw16 ? ((e2 & 0xFFFF) == key16 ? (int)(e2 >> 16) : 0) : s.lay3(KD & 0xFF);
+	const uint32_t T8 = (b1 + 1u) * 8u;             // (hdr_ext_len + 1) * 8
+
+	// HBH / DestOpts: opt_len = T8 - 2 <= pkt_len after the 2-byte pull;
+	// Routing: data_len = T8 - 4 <= pkt_len after the 4-byte pull
+	const bool t8ok = T8 <= len;
+	// IPv4: options pulled if present, else data stays (proto_ipv4.c:136)
+	const uint32_t ihl = b0 & 0xF;
+	const uint32_t opts = (ihl > 5 ? ihl : 5) * 4u - 20u;
+	const uint32_t v4adv = 20 + (opts <= len - 20 ? opts : 0);
+	// AH: hdr_len = plen*4 + 8, checked after the 12-byte pull, ICV pulled
+	const uint32_t hl = b1 * 4u + 8u;
+	const bool ahok = hl <= len - 12;
+	const uint32_t ahadv = 12 + ((ahok & (hl > 12)) ? hl - 12 : 0);
+	// Mobility: msg_len check, then (PRINT_NORM) get_mh_type's subtype pull
+	// and the second check
+	const int32_t mdl0 = (int32_t)T8 - 6;
+	const uint32_t l0 = len - 6;
+	const bool mok1 = mdl0 <= (int32_t)l0;
+	const uint32_t sub = b2 < 8 ? (uint32_t)(NSD_MH_SUB >> (8 * b2)) & 0xFF : 0u;
+	const bool sok = sub <= l0;
+	const uint32_t sp = sok ? sub : 0u;
+	const int32_t mdl = mdl0 - ((sok | (b2 <= 5)) ? (int32_t)sub : 0);
+	const bool mok2 = (mdl <= (int32_t)(l0 - sp)) & (mdl >= 0);
+	const bool mobok = MODE == PRINT_NORM ? mok1 & mok2 : mok1;
+	const uint32_t mobadv = !mok1 ? 6u : MODE != PRINT_NORM ? T8 : mok2 ? 6 + sp + (uint32_t)mdl : 6 + sp;
+	// ICMPv6 (PRINT_NORM): types 130-154 have variable-length bodies (host
+	// renders); types 1-4 / 128 / 129 pull a 4-byte body
+	const bool i6host = MODE == PRINT_NORM && b0 - 130u <= 24u;
+	const bool i6body = MODE == PRINT_NORM && ((b0 - 1u <= 3u) | ((b0 & 0xFE) == 128)) & (len >= 8);
+	const uint32_t i6adv = i6host ? 0u : i6body ? 8u : 4u;
+	uint32_t adv = fadv;
+	adv = kind == K_T8 ? (t8ok ? T8 : minl) : adv;
+	adv = kind == K_AH ? ahadv : adv;
+	adv = kind == K_IPV4 ? v4adv : adv;
+	adv = kind == K_MOB ? mobadv : adv;
+	adv = kind == K_ICMP6 ? i6adv : adv;
+	const bool cont = (kind == K_CONT) | (kind == K_IPV4) | ((kind == K_T8) & t8ok) |
+			  ((kind == K_AH) & ahok) | ((kind == K_MOB) & mobok);
+	const bool pulled = len >= minl;
+	const bool host = pulled & ((kind == K_HOST) | ((kind == K_ICMP6) & i6host));
+	const bool upd = act & (kind != K_MPLS);
+	w.data = upd ? start + (pulled ? adv : 0u) : w.data;
+	w.id = upd ? (pulled & cont ? nx : 0) : w.id;
+	w.flags |= upd & host ? NSD_F_HOST : 0;
+	if (MODE == PRINT_NORM) {
+		// tail trim to tot_len - ihl*4, evaluated in size_t (:174-175)
+		const int64_t x = (int64_t)k2 - (int64_t)ihl * 4;
+		const bool trim = upd & (kind == K_IPV4) & pulled & (x >= 0) & ((uint64_t)x < len - adv);
+		w.tail = trim ? start + adv + (uint32_t)x : w.tail;
+	}
+	// ---- the rare heavy bodies, behind wave-uniform branches
+	const bool v4 = upd && kind == K_IPV4 && pulled;
+	if (MODE == PRINT_NORM && __ballot(v4)) {
+		// checksum over ihl*4 bytes, past the frame too (bytes >= caplen are 0)
+		if (v4)
+			w.ip_csum = calc_csum(s, start, ihl * 2u);
+	}
+	const bool i4 = upd && id == NSD_OPS_ICMPV4 && pulled;
+	if (MODE == PRINT_NORM && __ballot(i4)) {
+		// calc_csum(icmp, pkt_len + 8): the whole (post-trim) message, odd
+		// trailing byte dropped (csum.h:24-27); past the window: pending
+		if (i4) {
+			if (s.in_window(start, len & ~1u)) {
+				if (calc_csum(s, start, len >> 1))
+					w.flags |= NSD_F_ICMP_BAD;
+			} else {
+				w.icmp_pend = true;
+				w.icmp_off = start;
+				w.icmp_len = len;
 			}
-			break;
-		case NSD_OPS_VLAN:          // proto_vlan.c:22-40
-		case NSD_OPS_QINQ:          // proto_vlan_q_in_q.c:23-41
-			if (len >= 4) {
-				next = lay2(s.be16(start + 2));
-				w.data = start + 4;
-			}
-			break;
-		case NSD_OPS_MPLS_UC: {     // proto_mpls_unicast.c:49-77
+		}
+	}
+	const bool mp = act && kind == K_MPLS;
+	if (__ballot(mp)) {                           // proto_mpls_unicast.c:49-77
+		if (mp) {
 			uint32_t d = start, l = len;
 			bool ok = true;
 			for (;;) {
 				if (l < 4) { ok = false; break; }
-				uint8_t sbit = s.b(d + 2) & 1;
+				const uint8_t sbit = s.b(d + 2) & 1;
 				d += 4; l -= 4;
 				if (sbit) break;
 			}
 			w.data = d;
+			int nxt = 0;
 			if (ok && l) {
-				uint8_t nib = s.b(d) >> 4;   // mpls_uc_next_proto :23-47
-				next = nib == 4 ? NSD_OPS_IPV4 : nib == 6 ? NSD_OPS_IPV6 : 0;
+				const uint8_t nib = s.b(d) >> 4;   // mpls_uc_next_proto :23-47
+				nxt = nib == 4 ? NSD_OPS_IPV4 : nib == 6 ? NSD_OPS_IPV6 : 0;
 			}
-			break;
+			w.id = nxt;
 		}
-		case NSD_OPS_IPV4: {        // proto_ipv4.c:34-178 / 180-204
-			if (len < 20)
-				break;
-			const uint8_t ihl = s.b(start) & 0xF;
-			const uint32_t proto = s.b(start + 9);
-			uint32_t d = start + 20, l = len - 20;
-			const uint32_t opts = (ihl > 5 ? ihl : 5) * 4u - 20u;
-			if (MODE == PRINT_NORM) {
-				// checksum over ihl*4 bytes, past the frame too (bytes >= caplen are 0)
-				w.ip_csum = calc_csum(s, start, ihl * 2u);
-			}
-			if (opts <= l) { d += opts; l -= opts; }
-			w.data = d;
-			if (MODE == PRINT_NORM) {
-				// trim to tot_len - ihl*4, evaluated in size_t (:174-175)
-				const int64_t x = (int64_t)s.be16(start + 2) - (int64_t)ihl * 4;
-				if (x >= 0 && (uint64_t)x < l)
-					w.tail = d + (uint32_t)x;
-			}
-			next = s.lay3(proto);
-			break;
-		}
-		case NSD_OPS_IPV6:          // proto_ipv6.c:22-105
-		case NSD_OPS_IPV6_IN_IPV4:  // proto_ipv6_in_ipv4.c:20-24
-			if (len >= 40) {
-				next = s.lay3(s.b(start + 6));
-				w.data = start + 40;
-			}
-			break;
-		case NSD_OPS_IPV6_HOP_BY_HOP:   // proto_ipv6_hop_by_hop.c:39-71
-		case NSD_OPS_IPV6_DEST_OPTS: {  // proto_ipv6_dest_opts.c:40-72
-			if (len < 2)
-				break;
-			const uint32_t opt_len = (s.b(start + 1) + 1u) * 8u - 2u;
-			w.data = start + 2;
-			if (opt_len <= len - 2) {
-				w.data += opt_len;
-				next = s.lay3(s.b(start));
-			}
-			break;
-		}
-		case NSD_OPS_IPV6_ROUTING: {    // proto_ipv6_routing.c:79-122
-			if (len < 4)
-				break;
-			const uint32_t data_len = (s.b(start + 1) + 1u) * 8u - 4u;
-			w.data = start + 4;
-			if (data_len <= len - 4) {
-				// type 0 pulls reserved + addresses, then the rest: same total
-				w.data += data_len;
-				next = s.lay3(s.b(start));
-			}
-			break;
-		}
-		case NSD_OPS_IPV6_FRAGM:    // proto_ipv6_fragm.c:25-47
-			if (len >= 8) {
-				next = s.lay3(s.b(start));
-				w.data = start + 8;
-			}
-			break;
-		case NSD_OPS_IP_AUTH: {     // proto_ip_authentication_hdr.c:26-69
-			if (len < 12)
-				break;
-			const uint32_t hdr_len = s.b(start + 1) * 4u + 8u;
-			w.data = start + 12;
-			if (hdr_len <= len - 12) {
-				if (hdr_len > 12)
-					w.data += hdr_len - 12;   // ICV bytes pulled one by one
-				next = s.lay3(s.b(start));
-			}
-			break;
-		}
-		case NSD_OPS_IP_ESP:        // proto_ip_esp.c:23-35: leaf
-			if (len >= 8)
-				w.data = start + 8;
-			break;
-		case NSD_OPS_IPV6_NO_NEXT:  // proto_ipv6_no_nxt_hdr.c:17-29: leaf, no pull
-			break;
-		case NSD_OPS_IPV6_MOBILITY: {   // proto_ipv6_mobility_hdr.c:247-309
-			if (len < 6)
-				break;
-			const int32_t hdr_ext_len = (s.b(start + 1) + 1) * 8;
-			int32_t mdl = hdr_ext_len - 6;
-			uint32_t d = start + 6, l = len - 6;
-			if (mdl > (int32_t)l)
-				{ w.data = d; break; }
-			if (MODE == PRINT_NORM) {
-				// get_mh_type (:206-245): subtype pull, then the length check
-				const uint8_t type = s.b(start + 2);
-				int32_t sub = 0;
-				bool dec_on_fail = true;
-				switch (type) {
-				case 0: sub = 2; break;
-				case 1: case 2: sub = 10; break;
-				case 3: case 4: sub = 18; break;
-				case 5: sub = 6; break;
-				case 6: sub = 6; dec_on_fail = false; break;
-				case 7: sub = 10; dec_on_fail = false; break;
-				}
-				if (sub) {
-					const bool ok = (uint32_t)sub <= l;
-					if (ok) { d += sub; l -= sub; }
-					if (ok || dec_on_fail)
-						mdl -= sub;
-				}
-				if (mdl > (int32_t)l || mdl < 0)
-					{ w.data = d; break; }
-			}
-			w.data = d + (uint32_t)mdl;
-			next = s.lay3(s.b(start));
-			break;
-		}
-		case NSD_OPS_TCP:           // proto_tcp.c:63-107: leaf, options not pulled
-			if (len >= 20)
-				w.data = start + 20;
-			break;
-		case NSD_OPS_UDP:           // proto_udp.c:23-58: leaf
-			if (len >= 8)
-				w.data = start + 8;
-			break;
-		case NSD_OPS_ICMPV4:        // proto_icmpv4.c:34-51: leaf
-			if (len >= 8) {
-				w.data = start + 8;
-				if (MODE == PRINT_NORM) {
-					// calc_csum(icmp, pkt_len + 8): the whole (post-trim)
-					// message, odd trailing byte dropped (csum.h:24-27).
-					// Short messages inside the staged window are summed
-					// here; longer ones by the whole wave afterwards.
-					if (s.in_window(start, len & ~1u)) {
-						if (calc_csum(s, start, len >> 1))
-							w.flags |= NSD_F_ICMP_BAD;
-					} else if constexpr (FAST) {
-						return true;
-					} else {
-						w.icmp_pend = true;
-						w.icmp_off = start;
-						w.icmp_len = len;
-					}
-				}
-			}
-			break;
-		case NSD_OPS_ICMPV6: {      // proto_icmpv6.c:1667-1699: leaf
-			if (len < 4)
-				break;
-			w.data = start + 4;
-			if (MODE == PRINT_NORM) {
-				const uint8_t type = s.b(start);
-				if (type >= 130 && type <= 154) {
-					// variable-length body (:372-911, :1023-1490): host renders
-					w.flags |= NSD_F_HOST;
-					w.data = start;
-				} else if ((type >= 1 && type <= 4) || type == 128 || type == 129) {
-					if (len - 4 >= 4)
-						w.data = start + 8;
-				}
-			}
-			break;
-		}
-		default:
-			// ARP, LLDP, IGMP, DCCP and non-Ethernet heads: host-rendered leaves
-			w.flags |= NSD_F_HOST;
-			w.data = start;
-			break;
-		}
-		if constexpr (FAST) {
-			if (s.missed())   // a byte outside the staged window was needed
-				return true;
-		}
-		w.id = next;
 	}
-	return false;
 }
 
 // Straight-line walk for the common chains (pass 1): Ethernet, up to two
