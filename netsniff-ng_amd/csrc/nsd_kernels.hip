@@ -31,9 +31,14 @@ namespace nsd {
 
 constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
-constexpr int WIN = 64;          // bytes per staged window
-constexpr int CPP = WIN / 16;    // 16-byte chunks per window
-constexpr int ROW = WIN / 4 + 1; // window row stride in dwords (odd: conflict-free reads)
+constexpr int WIN1 = 64;         // bytes per staged window, pass 1
+#ifndef NSD_WIN2
+#define NSD_WIN2 64
+#endif
+constexpr int WIN2 = NSD_WIN2;   // bytes per staged window, pass 2
+// window row stride in dwords (odd: 64 lanes reading the same offset hit 64
+// different banks)
+constexpr int row_of(int W) { return W / 4 + 1; }
 #ifndef NSD_CSUM_U
 #define NSD_CSUM_U 8               // interior chunk loads in flight per lane (dissect_icmp)
 #endif
@@ -58,7 +63,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
 // FAST: bytes outside the window are not fetched; the source records the
 // miss and the walk gives the packet up to pass 2.  Otherwise they come from
 // HBM (zero past caplen).
-template <bool FAST>
+template <bool FAST, int WIN>
 struct LSrc {
 	const uint32_t *win;     // this lane's window row
 	const uint8_t *lay3t;    // LDS copy of eth_lay3
@@ -80,7 +85,7 @@ struct LSrc {
 	{
 		const uint32_t r = o + m - wb;
 		uint32_t j = r >> 2;
-		j = j > 15 ? 15 : j;
+		j = j > WIN / 4 - 1 ? WIN / 4 - 1 : j;
 		const uint32_t v = __builtin_amdgcn_alignbyte(dw(j + 1), dw(j), r & 3);
 		return o >= caplen ? 0u : v;
 	}
@@ -118,7 +123,7 @@ struct LSrc {
 	{
 		const uint32_t r = o + m - wb;
 		uint32_t j = r >> 2;
-		j = j > 15 ? 15 : j;
+		j = j > WIN / 4 - 1 ? WIN / 4 - 1 : j;
 		const uint32_t sh = r & 3;
 		const uint32_t w0 = dw(j), w1 = dw(j + 1), w2 = dw(j + 2), w3 = dw(j + 3), w4 = dw(j + 4);
 		const bool z = o >= caplen;
@@ -162,10 +167,12 @@ struct LSrc {
 // loads chunk c of packet q's window, so the CPP chunks of one packet are
 // read by consecutive lanes as one contiguous, 16-byte aligned segment.
 
-static_assert(CPP * 6 <= 32, "chunk valid counts must fit one word");
+template <int WIN>
 struct Chunks {
+	static constexpr int CPP = WIN / 16;   // 16-byte chunks per window
+	static_assert(CPP * 6 <= 64, "chunk valid counts must fit one word");
 	uint4 v[CPP];
-	uint32_t nv;   // valid bytes of chunk r (0..16) in bits 6r..6r+5
+	uint64_t nv;   // valid bytes of chunk r (0..16) in bits 6r..6r+5
 };
 
 // issue the loads (no wait): in round r, lane (q * CPP + c) % 64 loads chunk
@@ -175,10 +182,11 @@ struct Chunks {
 // of valid bytes per chunk is kept for stage_write, which then needs no
 // shuffles.  my_wbp: window base (multiple of 16) | 0x80000000 when not
 // participating; without WB every packet with caplen > 0 participates at 0.
-template <bool WB>
-__device__ __forceinline__ void stage_load(Chunks &ch, const uint8_t *frames, uint64_t my_desc,
+template <bool WB, int WIN>
+__device__ __forceinline__ void stage_load(Chunks<WIN> &ch, const uint8_t *frames, uint64_t my_desc,
 					   uint32_t my_wbp, int lane)
 {
+	constexpr int CPP = Chunks<WIN>::CPP;
 	ch.nv = 0;
 #pragma unroll
 	for (int r = 0; r < CPP; r++) {
@@ -197,19 +205,21 @@ __device__ __forceinline__ void stage_load(Chunks &ch, const uint8_t *frames, ui
 		const uint32_t nv = part && pos < lim ? min(lim - pos, 16u) : 0u;
 		const uint64_t off = ((uint64_t)(dhi & 0xFF) << 32) | dlo;
 		ch.v[r] = nv ? *(const uint4 *)(frames + (off & ~15ull) + pos) : make_uint4(0, 0, 0, 0);
-		ch.nv |= nv << (6 * r);
+		ch.nv |= (uint64_t)nv << (6 * r);
 	}
 }
 
 // write the chunks to the window rows (row q, dwords 4c..4c+3), zeroing the
 // bytes at frame offsets >= caplen
-__device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks &ch, int lane)
+template <int WIN>
+__device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks<WIN> &ch, int lane)
 {
+	constexpr int CPP = Chunks<WIN>::CPP, ROW = row_of(WIN);
 #pragma unroll
 	for (int r = 0; r < CPP; r++) {
 		const int t = r * 64 + lane;
 		const int q = t / CPP, c = t % CPP;
-		const uint32_t nv = (ch.nv >> (6 * r)) & 0x3F;
+		const uint32_t nv = (uint32_t)(ch.nv >> (6 * r)) & 0x3F;
 		uint32_t w[4] = { ch.v[r].x, ch.v[r].y, ch.v[r].z, ch.v[r].w };
 		if (nv < 16) {
 #pragma unroll
@@ -371,6 +381,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 	uint32_t *__restrict__ queue, uint32_t region, uint32_t *__restrict__ qblk,
 	uint64_t *__restrict__ pend, uint32_t *__restrict__ pcnt)
 {
+	constexpr int ROW = row_of(WIN1);
 	__shared__ uint32_t s_win[WAVES][64 * ROW];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
 	__shared__ uint8_t s_lay3[256];
@@ -412,8 +423,8 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 	// descriptors are in flight
 	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
 	uint64_t d1 = (base + stride + lane < n) ? desc[base + stride + lane] : 0;
-	Chunks ch;
-	stage_load<false>(ch, frames, d0, 0, lane);
+	Chunks<WIN1> ch;
+	stage_load<false, WIN1>(ch, frames, d0, 0, lane);
 
 	for (; base < n; base += stride) {
 		const uint32_t i = base + lane;
@@ -427,14 +438,14 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
 		const uint32_t b1 = base + stride;
 		if (b1 < n)
-			stage_load<false>(ch, frames, d1, 0, lane);
+			stage_load<false, WIN1>(ch, frames, d1, 0, lane);
 		wave_sync_lds();
 
 		WalkOut w;
 		walk_init(w, caplen, valid ? start_id : 0);
 		bool deferred = false;
 		if (valid) {
-			const LSrc<true> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
+			const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
 					      (uint32_t)off & 15, 0, false };
 #ifdef NSD_X_NOWALK
 			w.chain = src.dw(3) & 0x3FF; w.n = 2; w.data = 42;
@@ -568,6 +579,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	const uint32_t *__restrict__ queue, uint32_t region, const uint32_t *__restrict__ qblk,
 	uint64_t *__restrict__ pend2, uint32_t *__restrict__ pcnt, ExtScr *__restrict__ scratch)
 {
+	constexpr int ROW = row_of(WIN2);
 	__shared__ uint32_t s_win[WAVES][64 * ROW];
 	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
 	__shared__ uint8_t s_lay3[256];
@@ -581,7 +593,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 		s_en = 0;
 	}
 	if (threadIdx.x < 64)
-		s_step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h[threadIdx.x - 32];
+		s_step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h.e[threadIdx.x - 32];
 	// (block_init's barrier orders these)
 	block_init(s_cnt, s_lay3);
 	uint64_t *const bp = pend2 + (size_t)blockIdx.x * region;   // this block's pending list
@@ -609,12 +621,12 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 		// lanes whose next header lies past their window suspend; the wave
 		// restages those windows at the lanes' cursors and resumes them
 		for (;;) {
-			Chunks ch;
+			Chunks<WIN2> ch;
 			const uint32_t wbp = wb | (part ? 0u : 0x80000000u);
-			stage_load<true>(ch, frames, d, wbp, lane);
+			stage_load<true, WIN2>(ch, frames, d, wbp, lane);
 			stage_write(&s_win[wv][0], ch, lane);
 			wave_sync_lds();
-			const LSrc<false> src{ &s_win[wv][lane * ROW], s_lay3, s_step, frames + off, caplen, m, wb,
+			const LSrc<false, WIN2> src{ &s_win[wv][lane * ROW], s_lay3, s_step, frames + off, caplen, m, wb,
 					       false };
 			bool susp;
 			for (;;) {
@@ -648,12 +660,14 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 		}
 		if (!valid)
 			continue;
+#ifndef NSD_X_NOEXT
 		if (w.ext_on) {
 			ExtScr *e = scr + w.slot;
 			e->pkt = i;
 			e->hdr = (w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS) |
 				 (uint32_t)(NSD_N_EXT | w.flags) << 16;   // the record's nflags, for ext_compact
 		}
+#endif
 		rec[i] = pack_record(w);
 		fc.add(w, caplen, true);
 	}
@@ -661,7 +675,9 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 	block_flush(s_cnt, counters);
 	if (threadIdx.x == 0)
 		pcnt[blockIdx.x * PLISTS + WAVES] = s_pn;   // ordered by block_flush's barrier
+#ifndef NSD_X_NOEXT
 	ext_compact(scr, s_en, s_ebase, rec, ext, ext_cap, ext_count, counters);
+#endif
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------

@@ -172,15 +172,21 @@ __constant__ uint32_t c_step[32] = {
 // general walk: slot ((key * 0x156) & 0xFFFF) >> 11 holds key | ops << 16
 // (one LDS read + compare instead of a 7-way compare tree)
 #define NSD_L2H(key) ((((key) * 0x156u) & 0xFFFFu) >> 11)
-__constant__ uint32_t c_lay2h[32] = {
-	[NSD_L2H(0x0806)] = 0x0806 | NSD_OPS_ARP << 16,
-	[NSD_L2H(0x88cc)] = 0x88cc | NSD_OPS_LLDP << 16,
-	[NSD_L2H(0x8100)] = 0x8100 | NSD_OPS_VLAN << 16,
-	[NSD_L2H(0x0800)] = 0x0800 | NSD_OPS_IPV4 << 16,
-	[NSD_L2H(0x86DD)] = 0x86DD | NSD_OPS_IPV6 << 16,
-	[NSD_L2H(0x88a8)] = 0x88a8 | NSD_OPS_QINQ << 16,
-	[NSD_L2H(0x8847)] = 0x8847 | NSD_OPS_MPLS_UC << 16,
+#define NSD_L2E(key, ops) (NSD_L2H(key) == i ? (key) | (ops) << 16 : 0u)
+struct Lay2Hash {
+	uint32_t e[32];
+	constexpr Lay2Hash() : e()
+	{
+		for (uint32_t i = 0; i < 32; i++)
+			e[i] = NSD_L2E(0x0806, NSD_OPS_ARP) | NSD_L2E(0x88cc, NSD_OPS_LLDP) |
+			       NSD_L2E(0x8100, NSD_OPS_VLAN) | NSD_L2E(0x0800, NSD_OPS_IPV4) |
+			       NSD_L2E(0x86DD, NSD_OPS_IPV6) | NSD_L2E(0x88a8, NSD_OPS_QINQ) |
+			       NSD_L2E(0x8847, NSD_OPS_MPLS_UC);
+	}
 };
+static_assert(NSD_L2H(0x0806) != NSD_L2H(0x88cc) && NSD_L2H(0x8100) != NSD_L2H(0x0800) &&
+	      NSD_L2H(0x86DD) != NSD_L2H(0x88a8), "eth_lay2 hash must be perfect");
+__constant__ Lay2Hash c_lay2h;
 
 // get_mh_type's subtype pull sizes for mobility types 0..7
 // (proto_ipv6_mobility_hdr.c:206-245), one byte per type
@@ -216,11 +222,13 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 		sb = __shfl(sb, leader, 64);
 		sb += __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0));
 		if (first) {
+#ifndef NSD_X_NOEXT
 			ExtScr *e = g.scr + sb;
 #pragma unroll
 			for (uint32_t j = 0; j < NSD_REC_MAX_LAYERS; j++)
 				if (j < k)
 					e->lay[j] = ((w.chain >> (5 * j)) & 31) | (uint32_t)off_of(w, j) << 16;
+#endif
 			w.slot = sb;
 			w.ext_on = true;
 		}
@@ -232,9 +240,13 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 	w.offB |= act && k >= 4 && k < NSD_REC_MAX_LAYERS ? (start & 0xFFFF) << (16 * (kk & 1)) : 0u;
 	w.flags |= act && k >= NSD_EXT_MAX_LAYERS && w.ext_on ? NSD_F_OVERFLOW : 0;
 	if (act && k < NSD_EXT_MAX_LAYERS) {
+#ifndef NSD_X_NOCNT
 		atomicAdd(&g.s_cnt[NSD_CNT_OPS + id], 1ull);   // the oracle counts the first 64 layers
+#endif
+#ifndef NSD_X_NOEXT
 		if (w.ext_on)
 			g.scr[w.slot].lay[k] = (uint32_t)id | start << 16;
+#endif
 	}
 	w.n = act ? k + 1 : k;
 
@@ -296,8 +308,8 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 	const bool host = pulled & ((kind == K_HOST) | ((kind == K_ICMP6) & i6host));
 	const bool upd = act & (kind != K_MPLS);
 	w.data = upd ? start + (pulled ? adv : 0u) : w.data;
-	w.id = upd ? (pulled & cont ? nx : 0) : w.id;
-	w.flags |= upd & host ? NSD_F_HOST : 0;
+	w.id = upd ? ((pulled & cont) ? nx : 0) : w.id;
+	w.flags |= (upd & host) ? NSD_F_HOST : 0;
 	if (MODE == PRINT_NORM) {
 		// tail trim to tot_len - ihl*4, evaluated in size_t (:174-175)
 		const int64_t x = (int64_t)k2 - (int64_t)ihl * 4;
