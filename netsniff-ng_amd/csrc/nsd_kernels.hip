@@ -289,6 +289,20 @@ __device__ __forceinline__ uint16_t csum_final(uint32_t sum)
 	return (uint16_t)~sum;
 }
 
+// Streaming record store: nontemporal (written once, read by the host or a
+// later kernel), measured 6 % faster than a plain store in the pass-1 access
+// shape (tools/bw: 72 B read + 16 B written per packet).
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_rec(uint4 *rec, uint32_t i, uint4 r)
+{
+#ifdef NSD_X_PLAINREC
+	rec[i] = r;
+#else
+	const v4u v = { r.x, r.y, r.z, r.w };
+	__builtin_nontemporal_store(v, (v4u *)(rec + i));
+#endif
+}
+
 // record words of a finished walk (layout of nsd_rec)
 __device__ __forceinline__ uint4 pack_record(const WalkOut &w)
 {
@@ -373,25 +387,38 @@ __device__ __forceinline__ uint64_t pend_entry(uint32_t i, uint32_t off, uint32_
 	return (uint64_t)i | (uint64_t)(off & 0xFFFF) << 32 | (uint64_t)(len & 0xFFFF) << 48;
 }
 
+// ---- the fused kernel ---------------------------------------------------------
+// Block-level shared state of one dissect launch.
+constexpr int WINMAX = WIN1 > WIN2 ? WIN1 : WIN2;
+struct Shared {
+	uint32_t win[WAVES][64 * row_of(WINMAX)];   // staged windows (pass 1, then pass 2)
+	unsigned long long cnt[NSD_NCOUNTERS];      // block counters
+	uint8_t lay3[256];                          // eth_lay3
+	uint32_t step[64];                          // c_step, c_lay2h (general walk)
+	uint32_t qn;                                // pass-1 deferrals queued
+	uint32_t pn;                                // pass-2 pending checksums
+	uint32_t en, ebase;                         // ext scratch entries, their global base
+	uint32_t pcnt[WAVES];                       // pass-1 pending checksums per wave
+};
+
 // ---- pass 1 ------------------------------------------------------------------
+// Every packet of the block's grid-stride tiles; packets whose chain does
+// not resolve inside their first 64 bytes are appended to the block's queue
+// (s_qn entries), ICMPv4 messages past the window to the wave's pending list
+// (s_pcnt[wave] entries).
 template <int MODE>
-__global__ __launch_bounds__(BLOCK) void dissect_fast(
-	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n,
-	int start_id, uint4 *__restrict__ rec, unsigned long long *__restrict__ counters,
-	uint32_t *__restrict__ queue, uint32_t region, uint32_t *__restrict__ qblk,
-	uint64_t *__restrict__ pend, uint32_t *__restrict__ pcnt)
+__device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ frames,
+				      const uint64_t *__restrict__ desc, uint32_t n, int start_id,
+				      uint4 *__restrict__ rec, uint32_t *__restrict__ queue, uint32_t region,
+				      uint64_t *__restrict__ pend)
 {
 	constexpr int ROW = row_of(WIN1);
-	__shared__ uint32_t s_win[WAVES][64 * ROW];
-	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
-	__shared__ uint8_t s_lay3[256];
-	__shared__ uint32_t s_qn;
-
+	auto &s_win = sh.win;
+	auto &s_qn = sh.qn;
+	unsigned long long *const s_cnt = sh.cnt;
+	const uint8_t *const s_lay3 = sh.lay3;
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
-	if (threadIdx.x == 0)
-		s_qn = 0;
-	block_init(s_cnt, s_lay3);
 
 	const uint32_t stride = gridDim.x * BLOCK;
 	uint32_t *const bq = queue + (size_t)blockIdx.x * region;   // this block's queue region
@@ -408,14 +435,11 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 			fc.pkts += FlagCnt::pc(i < n);
 			if (i < n) {
 				const uint32_t caplen = NSD_DESC_CAPLEN(desc[i]);
-				rec[i] = make_uint4(0, caplen << 16, 0, 0);
+				store_rec(rec, i, make_uint4(0, caplen << 16, 0, 0));
 				fc.bytes += caplen;
 			}
 		}
 		fc.flush(s_cnt, lane);
-		block_flush(s_cnt, counters);
-		if (threadIdx.x == 0)
-			qblk[blockIdx.x] = 0;
 		return;
 	}
 
@@ -455,7 +479,7 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 		}
 		wave_sync_lds();
 		if (MODE == PRINT_NORM) {
-			// ICMPv4 messages past the window: listed for dissect_icmp, which
+			// ICMPv4 messages past the window: listed for the checksum pass, which
 			// patches the record if the sum is bad
 			const bool pnd = w.icmp_pend && !deferred;
 			const uint64_t pmask = __ballot(pnd);
@@ -497,17 +521,14 @@ __global__ __launch_bounds__(BLOCK) void dissect_fast(
 			}
 		}
 		if (done)
-			rec[i] = pack_record(w);
+			store_rec(rec, i, pack_record(w));
 		fc.add(w, caplen, done);
 		d0 = d1;
 		d1 = d2;
 	}
 	if (lane == 0)
-		pcnt[blockIdx.x * PLISTS + wv] = npend;
+		sh.pcnt[wv] = npend;
 	fc.flush(s_cnt, lane);
-	block_flush(s_cnt, counters);
-	if (threadIdx.x == 0)
-		qblk[blockIdx.x] = s_qn;   // block_flush's barrier ordered every append before this
 }
 
 // Block end of pass 2: the block's scratch ext entries move to the caller's
@@ -571,38 +592,30 @@ __device__ __forceinline__ void ext_compact(const ExtScr *scr, uint32_t &s_en, u
 }
 
 // ---- pass 2 ------------------------------------------------------------------
+// The packets pass 1 queued (the block's own queue region), walked from
+// scratch with the resumable general walk; ICMPv4 messages past the window go
+// to the block's pass-2 pending list (s_pn entries), ext chains to the
+// block's scratch (s_en entries, compacted by ext_compact).
 template <int MODE>
-__global__ __launch_bounds__(BLOCK) void dissect_general(
-	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, int start_id,
-	uint4 *__restrict__ rec, nsd_ext *__restrict__ ext, uint32_t ext_cap,
-	uint32_t *__restrict__ ext_count, unsigned long long *__restrict__ counters,
-	const uint32_t *__restrict__ queue, uint32_t region, const uint32_t *__restrict__ qblk,
-	uint64_t *__restrict__ pend2, uint32_t *__restrict__ pcnt, ExtScr *__restrict__ scratch)
+__device__ __forceinline__ void pass2(Shared &sh, const uint8_t *__restrict__ frames,
+				      const uint64_t *__restrict__ desc, int start_id, uint4 *__restrict__ rec,
+				      const uint32_t *__restrict__ queue, uint32_t region,
+				      uint64_t *__restrict__ pend2, ExtScr *__restrict__ scratch)
 {
 	constexpr int ROW = row_of(WIN2);
-	__shared__ uint32_t s_win[WAVES][64 * ROW];
-	__shared__ unsigned long long s_cnt[NSD_NCOUNTERS];
-	__shared__ uint8_t s_lay3[256];
-	__shared__ uint32_t s_pn, s_en, s_ebase;
-	__shared__ uint32_t s_step[64];   // c_step, c_lay2h
-
+	auto &s_win = sh.win;
+	auto &s_pn = sh.pn;
+	unsigned long long *const s_cnt = sh.cnt;
+	const uint8_t *const s_lay3 = sh.lay3;
+	const uint32_t *const s_step = sh.step;
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
-	if (threadIdx.x == 0) {
-		s_pn = 0;
-		s_en = 0;
-	}
-	if (threadIdx.x < 64)
-		s_step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h.e[threadIdx.x - 32];
-	// (block_init's barrier orders these)
-	block_init(s_cnt, s_lay3);
 	uint64_t *const bp = pend2 + (size_t)blockIdx.x * region;   // this block's pending list
 
-	// block b drains the queue region pass 1's block b filled
-	const uint32_t nq = qblk[blockIdx.x];
+	const uint32_t nq = sh.qn;
 	const uint32_t *const bq = queue + (size_t)blockIdx.x * region;
 	ExtScr *const scr = scratch + (size_t)blockIdx.x * region;   // this block's ext scratch
-	const GenSink g{ scr, &s_en, s_cnt };
+	const GenSink g{ scr, &sh.en, s_cnt };
 	FlagCnt fc;
 
 	for (uint32_t base = wv * 64; base < nq; base += BLOCK) {
@@ -668,20 +681,14 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 				 (uint32_t)(NSD_N_EXT | w.flags) << 16;   // the record's nflags, for ext_compact
 		}
 #endif
-		rec[i] = pack_record(w);
+		store_rec(rec, i, pack_record(w));
 		fc.add(w, caplen, true);
 	}
 	fc.flush(s_cnt, lane);
-	block_flush(s_cnt, counters);
-	if (threadIdx.x == 0)
-		pcnt[blockIdx.x * PLISTS + WAVES] = s_pn;   // ordered by block_flush's barrier
-#ifndef NSD_X_NOEXT
-	ext_compact(scr, s_en, s_ebase, rec, ext, ext_cap, ext_count, counters);
-#endif
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
-// Runs after both passes (the records are final): block b's waves take b's
+// Runs after both passes (the records are final): the block's waves take its
 // lists in 64-entry pieces and patch the flags byte of the records whose sum
 // is bad.  Four lanes per message, 16 messages per wave at a time: lane
 // `sub` of a group sums the interior chunks 1 + sub + 4t (whole 16-byte
@@ -690,25 +697,21 @@ __global__ __launch_bounds__(BLOCK) void dissect_general(
 // and last chunk with the bytes outside the message masked.  A message then
 // costs a few wave instructions per KiB instead of one wave per message.
 template <int U>
-__global__ __launch_bounds__(BLOCK) void dissect_icmp(
-	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint4 *__restrict__ rec,
-	unsigned long long *__restrict__ counters, const uint64_t *__restrict__ pend,
-	const uint64_t *__restrict__ pend2, uint32_t region, const uint32_t *__restrict__ pcnt,
-	uint32_t split)
+__device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict__ frames,
+					  const uint64_t *__restrict__ desc, uint4 *__restrict__ rec,
+					  const uint64_t *__restrict__ pend, const uint64_t *__restrict__ pend2,
+					  uint32_t region)
 {
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
 	const uint32_t sub = lane & 3, grp = lane >> 2;
-	// `split` blocks share the lists of one pass-1 block
-	const uint32_t ob = blockIdx.x / split, part = blockIdx.x % split;
-	const uint32_t nw = WAVES * split, w0 = part * WAVES + wv;
 	uint32_t bad = 0;
 	for (int l = 0; l < PLISTS; l++) {
-		const uint32_t cnt = pcnt[ob * PLISTS + l];
-		const uint64_t *list = l < WAVES ? pend + ((size_t)ob * WAVES + l) * (region / WAVES)
-						 : pend2 + (size_t)ob * region;
-		// the waves of the `split` blocks split each list in 64-entry pieces
-		for (uint32_t k0 = 64 * ((w0 + l) % nw); k0 < cnt; k0 += 64 * nw) {
+		const uint32_t cnt = l < WAVES ? sh.pcnt[l] : sh.pn;
+		const uint64_t *list = l < WAVES ? pend + ((size_t)blockIdx.x * WAVES + l) * (region / WAVES)
+						 : pend2 + (size_t)blockIdx.x * region;
+		// the block's waves split each list in 64-entry pieces
+		for (uint32_t k0 = 64 * ((wv + l) % WAVES); k0 < cnt; k0 += 64 * WAVES) {
 			const bool on = k0 + lane < cnt;
 			const uint64_t e = on ? list[k0 + lane] : 0;
 			const uint32_t i = (uint32_t)e;
@@ -759,16 +762,59 @@ __global__ __launch_bounds__(BLOCK) void dissect_icmp(
 		}
 	}
 	if (lane == 0 && bad)
-		atomicAdd(&counters[NSD_CNT_ICMP_BAD], (unsigned long long)bad);
+		atomicAdd(&sh.cnt[NSD_CNT_ICMP_BAD], (unsigned long long)bad);
+}
+
+// One launch per batch.  Each block of the persistent grid runs, in order:
+// pass 1 over its grid-stride tiles, pass 2 over the packets it queued, the
+// ext compaction, and the ICMPv4 checksums it left pending.  Every later
+// phase reads only what the same block wrote (its queue region, pending lists
+// and scratch), so the phases need block barriers, not grid-wide ones, and a
+// block's pass 2 / checksum work overlaps other blocks' pass 1.
+template <int MODE>
+__global__ __launch_bounds__(BLOCK, 5) void dissect_all(
+	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
+	uint4 *__restrict__ rec, nsd_ext *__restrict__ ext, uint32_t ext_cap,
+	uint32_t *__restrict__ ext_count, unsigned long long *__restrict__ counters,
+	uint32_t *__restrict__ queue, uint32_t region, uint64_t *__restrict__ pend,
+	uint64_t *__restrict__ pend2, ExtScr *__restrict__ scratch)
+{
+	__shared__ Shared sh;
+	if (threadIdx.x == 0) {
+		sh.qn = 0;
+		sh.pn = 0;
+		sh.en = 0;
+	}
+	if (threadIdx.x < 64)
+		sh.step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h.e[threadIdx.x - 32];
+	block_init(sh.cnt, sh.lay3);   // (its barrier orders the stores above too)
+
+	pass1<MODE>(sh, frames, desc, n, start_id, rec, queue, region, pend);
+	if (MODE == PRINT_NORM || MODE == PRINT_LESS) {
+		__syncthreads();   // the block's queue and sh.qn are complete
+#ifndef NSD_X_NOP2
+		pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, scratch);
+#endif
+#ifndef NSD_X_NOEXT
+		ext_compact(scratch + (size_t)blockIdx.x * region, sh.en, sh.ebase, rec, ext, ext_cap,
+			    ext_count, counters);   // (starts with a barrier)
+#endif
+	}
+	if (MODE == PRINT_NORM) {
+		__syncthreads();   // records final, pending lists and counts complete
+#ifndef NSD_X_NOICMP
+		icmp_pass<NSD_CSUM_U>(sh, frames, desc, rec, pend, pend2, region);
+#endif
+	}
+	block_flush(sh.cnt, counters);
 }
 
 } // namespace nsd
 
-// ---- launchers (C ABI, called by nsd_host.cpp) ------------------------------
-// Pass 1 runs a persistent grid of at most NSD_MAX_GRID blocks; block b owns
-// queue region b (room for every packet it visits) and writes its deferred
-// count to qblk[b]; pass 2 runs the same grid, block b draining region b.
-// workspace: qblk[NSD_MAX_GRID] u32, then the regions.
+// ---- launcher (C ABI, called by nsd_host.cpp / nsd_pipe.cpp) -----------------
+// A persistent grid of at most NSD_MAX_GRID blocks; block b owns queue
+// region b, pending lists b and ext scratch b (room for every packet it
+// visits).
 constexpr uint32_t NSD_MAX_GRID = 4096;
 
 static uint32_t region_for(uint32_t n, uint32_t blocks)
@@ -783,12 +829,12 @@ static size_t region_slots(uint32_t n)
 	return ((size_t)n + (size_t)NSD_MAX_GRID * nsd::BLOCK + 1) & ~(size_t)1;
 }
 
-// workspace: qblk[NSD_MAX_GRID], pcnt[NSD_MAX_GRID * 8], the deferral queue
-// (u32 per slot), the pass-1 and pass-2 pending-checksum lists (u64 per slot),
-// pass 2's per-block ext scratch (ExtScr per slot, 16-byte aligned)
+// workspace: the deferral queue (u32 per slot), the pass-1 and pass-2
+// pending-checksum lists (u64 per slot), the per-block ext scratch (ExtScr
+// per slot, 16-byte aligned)
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
-	return 4 * (size_t)NSD_MAX_GRID * 9 + 16 + (4 + 8 + 8 + sizeof(nsd::ExtScr)) * region_slots(n);
+	return 16 + (4 + 8 + 8 + sizeof(nsd::ExtScr)) * region_slots(n);
 }
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
@@ -809,14 +855,14 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	const uint32_t waves = (n + 63) / 64;
 	uint32_t blocks = (waves + WAVES - 1) / WAVES;
 	// persistent grid: exactly the blocks that are resident together (CUs x
-	// the pass-1 kernel's occupancy), so no block waits for a second round;
-	// every block grid-strides (counters then cost one flush per block)
+	// the kernel's occupancy), so no block waits for a second round; every
+	// block grid-strides (counters then cost one flush per block)
 	static int s_occ[3] = { 0, 0, 0 };
 	const int mi = mode == PRINT_NORM ? 0 : mode == PRINT_LESS ? 1 : 2;
+	const void *f = mi == 0 ? (const void *)dissect_all<PRINT_NORM>
+		      : mi == 1 ? (const void *)dissect_all<PRINT_LESS>
+				: (const void *)dissect_all<PRINT_HEX>;
 	if (!s_occ[mi]) {
-		const void *f = mi == 0 ? (const void *)dissect_fast<PRINT_NORM>
-			      : mi == 1 ? (const void *)dissect_fast<PRINT_LESS>
-					: (const void *)dissect_fast<PRINT_HEX>;
 		int occ = 0;
 		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, BLOCK, 0) != hipSuccess || occ < 1)
 			occ = 4;
@@ -828,35 +874,13 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	if (blocks > cap_blocks)
 		blocks = cap_blocks;
 	const uint32_t region = region_for(n, blocks);
-	unsigned long long *cnt = (unsigned long long *)d_counters;
-	uint4 *rec = (uint4 *)d_rec;
-	uint32_t *qblk = (uint32_t *)d_ws;
-	uint32_t *pcnt = qblk + NSD_MAX_GRID;
-	uint32_t *queue = pcnt + 8 * NSD_MAX_GRID;
+	uint32_t *queue = (uint32_t *)d_ws;
 	uint64_t *pend = (uint64_t *)(queue + region_slots(n));
 	uint64_t *pend2 = pend + region_slots(n);
 	ExtScr *scratch = (ExtScr *)(((uintptr_t)(pend2 + region_slots(n)) + 15) & ~(uintptr_t)15);
-	switch (mode) {
-	case PRINT_NORM:
-		hipLaunchKernelGGL(dissect_fast<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend, pcnt);
-		hipLaunchKernelGGL(dissect_general<PRINT_NORM>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
-				   region, qblk, pend2, pcnt, scratch);
-		hipLaunchKernelGGL(dissect_icmp<NSD_CSUM_U>, dim3(blocks * NSD_CSUM_SPLIT), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, rec, cnt, pend, pend2, region, pcnt, (uint32_t)NSD_CSUM_SPLIT);
-		break;
-	case PRINT_LESS:
-		hipLaunchKernelGGL(dissect_fast<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend, pcnt);
-		hipLaunchKernelGGL(dissect_general<PRINT_LESS>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, start_id, rec, d_ext, ext_cap, d_ext_count, cnt, queue,
-				   region, qblk, pend2, pcnt, scratch);
-		break;
-	default:
-		hipLaunchKernelGGL(dissect_fast<PRINT_HEX>, dim3(blocks), dim3(BLOCK), 0, stream,
-				   d_frames, d_desc, n, start_id, rec, cnt, queue, region, qblk, pend, pcnt);
-		break;
-	}
+	hipLaunchKernelGGL(mi == 0 ? dissect_all<PRINT_NORM> : mi == 1 ? dissect_all<PRINT_LESS> : dissect_all<PRINT_HEX>,
+			   dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id,
+			   (uint4 *)d_rec, d_ext, ext_cap, d_ext_count, (unsigned long long *)d_counters,
+			   queue, region, pend, pend2, scratch);
 	return hipGetLastError() == hipSuccess ? 0 : -2;
 }
