@@ -104,7 +104,7 @@ typedef uint64_t nsd_desc_t;
  *           (calc_csum over ihl*4 bytes, proto_ipv4.c:51); 0 means "ok".
  *           Only computed in PRINT_NORM; 0 otherwise.
  * nflags  : bits 0..2 = number of layers run (0..6), 7 = NSD_N_EXT (the full
- *           chain is in the ext table, slot = off2[0..3] little-endian u32);
+ *           chain is in the ext pool, slot = off2[0..3] little-endian u32);
  *           bits 3..7 = NSD_F_* flags.
  * off2[k-1]: start offset of layer k divided by 2, k = 1..5 (layer 0 starts
  *           at 0). Every layer start is even, and offsets > 510
@@ -124,22 +124,39 @@ typedef struct nsd_rec {
 #define NSD_F_ICMP_BAD       0x08  /* ICMPv4 checksum nonzero: "bogus (!)" (proto_icmpv4.c:74-81) */
 #define NSD_F_HOST           0x10  /* last layer's body is rendered by the host (ICMPv6 130-154,
                                       ARP, LLDP, IGMP, DCCP, non-Ethernet link types) */
-#define NSD_F_OVERFLOW       0x20  /* chain longer than NSD_EXT_MAX_LAYERS or ext table full:
+#define NSD_F_OVERFLOW       0x20  /* chain longer than NSD_EXT_MAX_LAYERS or ext pool full:
                                       record holds the first layers only */
 
 #define NSD_REC_NLAYERS(r)   ((r)->nflags & 7u)
 #define NSD_REC_ID(r, k)     (((r)->chain >> (5u * (k))) & 31u)
 
-/* Overflow ("ext") record for chains longer than 6 layers or with a layer
- * starting past byte 510.  Slots are taken with a wave-aggregated atomic. */
+/* ---- ext pool: chains the 16-byte record cannot hold --------------------
+ * Chains longer than NSD_REC_MAX_LAYERS layers, or with a layer starting past
+ * byte 510, keep their full layer list in a pool of u32 words; the record's
+ * slot (off2[0..3], little-endian) is the entry's word index s:
+ *   pool[s + 0]     packet index within the batch
+ *   pool[s + 1]     nlayers
+ *   pool[s + 2..3]  reserved
+ *   pool[s + 4 + k] ops ID (bits 0..7) | start offset of layer k (bits 16..31),
+ *                   k < nlayers (at most NSD_EXT_MAX_LAYERS)
+ * An entry occupies NSD_EXT_WORDS(nlayers) words.  The device hands pool
+ * words out in per-wave chunks, so *ext_used (the words handed out) can
+ * exceed the words holding entries; an entry that does not fit in the pool
+ * leaves its record with NSD_F_OVERFLOW and slot 0xFFFFFFFF.  Entry order is
+ * unspecified (follow the records' slots).  Sizing: the unused chunk tails
+ * cost at most half the pool, so a pool of twice the words the batch's
+ * chains need never overflows; NSD_EXT_POOL_WORDS(n) is that for n packets
+ * whose chains are at most 16 layers, plus room for a few deeper ones.
+ * Pools are capped at NSD_EXT_POOL_MAX_WORDS words. */
 #define NSD_EXT_MAX_LAYERS   64
-typedef struct nsd_ext {
-	uint32_t pkt;                      /* packet index within the batch */
-	uint16_t nlayers;
-	uint16_t rsvd;
-	uint8_t  id[NSD_EXT_MAX_LAYERS];
-	uint16_t off[NSD_EXT_MAX_LAYERS];  /* start offset of each layer */
-} nsd_ext;                             /* 200 bytes */
+#define NSD_EXT_HDR_WORDS    4u
+#define NSD_EXT_WORDS(nl)    ((nl) <= 16u ? NSD_EXT_HDR_WORDS + 16u : NSD_EXT_HDR_WORDS + NSD_EXT_MAX_LAYERS)
+#define NSD_EXT_POOL_WORDS(n)   (48ull * (n) + 4096u)
+#define NSD_EXT_POOL_MAX_WORDS  0xF0000000u
+#define NSD_EXT_PKT(pool, s)      ((pool)[(s)])
+#define NSD_EXT_NLAYERS(pool, s)  ((pool)[(s) + 1] & 0xFFFFu)
+#define NSD_EXT_ID(pool, s, k)    ((pool)[(s) + NSD_EXT_HDR_WORDS + (k)] & 0xFFu)
+#define NSD_EXT_OFF(pool, s, k)   ((pool)[(s) + NSD_EXT_HDR_WORDS + (k)] >> 16)
 
 /* ---- per-protocol counter vector (u64, summed over the batch) ----------- */
 enum nsd_counter {
@@ -149,7 +166,7 @@ enum nsd_counter {
 	NSD_CNT_IP_BAD    = 34,  /* IPv4 header checksum bogus (PRINT_NORM) */
 	NSD_CNT_ICMP_BAD  = 35,  /* ICMPv4 checksum bogus (PRINT_NORM) */
 	NSD_CNT_HOST      = 36,  /* records flagged NSD_F_HOST */
-	NSD_CNT_EXT       = 37,  /* records using the ext table */
+	NSD_CNT_EXT       = 37,  /* records using the ext pool */
 	NSD_CNT_OVERFLOW  = 38,  /* records flagged NSD_F_OVERFLOW */
 	NSD_CNT_TRIM      = 39,  /* IPv4 tail trims (tail_off < caplen) */
 	NSD_NCOUNTERS     = 64
@@ -175,41 +192,45 @@ int  dissector_set_print_type(void *ptr, int type);
 
 /* Device-resident walk: every pointer is device memory, the call only
  * enqueues work on `stream` (no host synchronisation, graph-capturable).
- * `d_counters` (NSD_NCOUNTERS u64) is accumulated into, not overwritten;
- * `d_ext_count` (one u32) likewise.  `mode` selects the parse semantics
- * (print_full vs print_less chains differ, SURVEY §8a quirk 7 / mobility).
- * Returns NSD_OK or an error without launching. */
+ * `d_ext` is the ext pool of `ext_words` u32 words (may be NULL when 0);
+ * `d_ext_used` (one u32, the pool words handed out) is a running offset: set
+ * it to 0 before a batch that starts a fresh pool.  `d_counters`
+ * (NSD_NCOUNTERS u64) is accumulated into, not overwritten.  `mode` selects
+ * the parse semantics (print_full vs print_less chains differ, SURVEY §8a
+ * quirk 7 / mobility).  Returns NSD_OK or an error without launching. */
 int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
 		       int linktype, int mode,
-		       nsd_rec *d_rec, nsd_ext *d_ext, uint32_t ext_cap,
-		       uint32_t *d_ext_count, uint64_t *d_counters, void *stream);
+		       nsd_rec *d_rec, uint32_t *d_ext, uint32_t ext_words,
+		       uint32_t *d_ext_used, uint64_t *d_counters, void *stream);
 
 /* Same, with a caller-provided device workspace of nsd_workspace_bytes(n)
- * bytes (the compaction queue between the fast and the general pass): no
- * allocation inside, so the call can be captured in a hipGraph.
+ * bytes (the deferral queue and pending-checksum lists between the kernel's
+ * phases): no allocation inside, so the call can be captured in a hipGraph.
  * nsd_dissect_device uses a library-owned workspace grown on demand. */
 size_t nsd_workspace_bytes(uint32_t n);
 int nsd_dissect_device_ws(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
-			  int linktype, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
-			  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+			  int linktype, int mode, nsd_rec *d_rec, uint32_t *d_ext,
+			  uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
 			  void *d_workspace, void *stream);
 
 /* Host-memory batch: stages frames/descriptors to HBM, runs
- * nsd_dissect_device, copies records/ext/counters back.  Synchronous.
- * `counters` may be NULL; `ext` may be NULL when ext_cap == 0. */
+ * nsd_dissect_device with a fresh pool, copies records / the used pool words
+ * / counters back.  Synchronous.  `counters` may be NULL; `ext` may be NULL
+ * when ext_words == 0; *ext_used (may be NULL) receives the pool words
+ * handed out. */
 int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
 			  const nsd_desc_t *desc, uint32_t n, int linktype, int mode,
-			  nsd_rec *rec, nsd_ext *ext, uint32_t ext_cap,
-			  uint32_t *ext_count, uint64_t *counters);
+			  nsd_rec *rec, uint32_t *ext, uint32_t ext_words,
+			  uint32_t *ext_used, uint64_t *counters);
 
 /* Host formatter: renders one record + its raw frame bytes into the exact
  * text the reference dissector chain prints (unwrapped tprintf stream, i.e.
  * what dissector_entry_point hands to tprintf for this packet).
- * `ext_table` is the ext array the record's slot refers to (may be NULL if
- * the record has no ext slot).  Writes at most `cap` bytes (NUL-terminated
- * when room), returns the full text length, or a negative NSD_ERR_*. */
+ * `ext_pool` is the pool the record's slot refers to (may be NULL if the
+ * record has no ext slot).  Writes at most `cap` bytes (NUL-terminated when
+ * room), returns the full text length, or a negative NSD_ERR_*. */
 long nsd_format_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-		       const nsd_rec *rec, const nsd_ext *ext_table,
+		       const nsd_rec *rec, const uint32_t *ext_pool,
 		       char *out, size_t cap);
 
 /* Name tables (lookup.c:33-95): load udp.conf / tcp.conf / ether.conf /
@@ -235,25 +256,61 @@ long nsd_tprintf_wrap(const char *in, size_t len, int cols, long *state,
  * asynchronous, pageable ones still work but serialise them.
  * Batches complete in submission order.
  *
- * nsd_pipe_create: capacities per batch (packets, frame bytes, ext slots),
+ * nsd_pipe_create: capacities per batch (packets, frame bytes, ext pool words),
  * 1 <= depth <= 8.  NULL on failure (no GPU, no memory, bad arguments).
  * nsd_pipe_submit: validates like dissector_entry_batch, then enqueues; when
  * all slots are busy it first completes the oldest batch (its status is
  * returned through that batch's *status, see below).  rec[n] receives the
- * records, ext[ext_cap] / *ext_count the spilled layers, counters[64] (may
+ * records, ext[ext_words] / *ext_used the ext pool, counters[64] (may
  * be NULL) this batch's counters, *status (may be NULL) the batch's final
  * status.  Returns NSD_OK if enqueued, else NSD_ERR_*.
  * nsd_pipe_wait: completes the oldest in-flight batch, returns its status,
  * or 1 when nothing is in flight.  nsd_pipe_drain: completes all. */
 typedef struct nsd_pipe nsd_pipe;
-nsd_pipe *nsd_pipe_create(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_cap,
+nsd_pipe *nsd_pipe_create(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_words,
 			  int depth, int linktype, int mode);
 int nsd_pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
-		    const nsd_desc_t *desc, uint32_t n, nsd_rec *rec, nsd_ext *ext,
-		    uint32_t *ext_count, uint64_t *counters, int *status);
+		    const nsd_desc_t *desc, uint32_t n, nsd_rec *rec, uint32_t *ext,
+		    uint32_t *ext_used, uint64_t *counters, int *status);
 int nsd_pipe_wait(nsd_pipe *p);
 int nsd_pipe_drain(nsd_pipe *p);
 void nsd_pipe_destroy(nsd_pipe *p);
+
+/* ---- classic BPF on the device --------------------------------
+ * The capture loop filters every record before dissecting it (read_pcap
+ * netsniff-ng.c:707-725: bpf_run_filter, bpf.c:508-705, skips the record on
+ * 0).  Programs are struct sock_filter arrays (linux/filter.h), as
+ * bpf_parse_rules (bpf.c:707-766) reads them.
+ *
+ * nsd_bpf_validate: __bpf_validate (bpf.c:388-506), 1 = valid, 0 = not.
+ * nsd_bpf_load: validates, decodes and uploads a program; NULL if it is
+ * invalid, longer than 4096 instructions (BPF_MAXINSNS), has a jump whose
+ * target leaves the program in 64-bit arithmetic (which __bpf_validate's
+ * 32-bit check lets through and the reference then runs off its program),
+ * or there is no device.
+ * nsd_bpf_filter_device: device pointers, enqueued on `stream`; d_verdict[i]
+ * = bpf_run_filter's return for packet i (0 = drop).  With d_desc_out (and
+ * d_count, d_workspace of nsd_bpf_workspace_bytes(n) bytes) the descriptors
+ * of the accepted packets are packed in batch order into d_desc_out and
+ * their number written to *d_count: the dissect kernels' input.
+ * nsd_bpf_filter_batch: host memory in and out, synchronous. */
+typedef struct nsd_bpf_insn {
+	uint16_t code;
+	uint8_t  jt;
+	uint8_t  jf;
+	uint32_t k;
+} nsd_bpf_insn;
+typedef struct nsd_bpf_prog nsd_bpf_prog;
+int nsd_bpf_validate(const nsd_bpf_insn *prog, uint32_t len);
+nsd_bpf_prog *nsd_bpf_load(const nsd_bpf_insn *prog, uint32_t len);
+void nsd_bpf_free(nsd_bpf_prog *prog);
+size_t nsd_bpf_workspace_bytes(uint32_t n);
+int nsd_bpf_filter_device(const nsd_bpf_prog *prog, const uint8_t *d_frames,
+			  const nsd_desc_t *d_desc, uint32_t n, uint32_t *d_verdict,
+			  nsd_desc_t *d_desc_out, uint32_t *d_count, void *d_workspace,
+			  void *stream);
+int nsd_bpf_filter_batch(const nsd_bpf_prog *prog, const uint8_t *frames, size_t frames_len,
+			 const nsd_desc_t *desc, uint32_t n, uint32_t *verdict);
 
 /* Pinned host memory for the pipe's buffers. */
 void *nsd_host_alloc(size_t len);

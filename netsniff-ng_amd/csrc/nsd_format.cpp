@@ -919,11 +919,13 @@ static void dump_hex(Out &o, const Frame &f, uint32_t from, uint32_t len)
 	o << " ]\n";
 }
 
+#include "nsd_format_leaves.h"
+
 static bool is_lt(int lt, uint32_t v) { return (uint32_t)lt == v || (uint32_t)lt == __builtin_bswap32(v); }
 
 // Render one packet; returns NSD_OK or NSD_ERR_FORMAT (text so far kept).
 int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-		  const nsd_rec &rec, const nsd_ext *ext_table)
+		  const nsd_rec &rec, const uint32_t *ext_pool)
 {
 	Out o(s);
 	Frame f{ pkt, caplen };
@@ -945,31 +947,31 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 
 	// the chain as the device recorded it
 	uint32_t n = rec.nflags & 7u;
-	const uint8_t *ids = nullptr;
-	const uint16_t *offs = nullptr;
-	uint8_t lid[NSD_REC_MAX_LAYERS];
-	uint16_t loff[NSD_REC_MAX_LAYERS];
+	uint8_t ids[NSD_EXT_MAX_LAYERS];
+	uint16_t offs[NSD_EXT_MAX_LAYERS];
 	if (n == NSD_N_EXT) {
 		uint32_t slot;
 		memcpy(&slot, rec.off2, 4);
-		if (!ext_table || slot == 0xFFFFFFFFu || (rec.nflags & NSD_F_OVERFLOW))
+		if (!ext_pool || slot == 0xFFFFFFFFu || (rec.nflags & NSD_F_OVERFLOW))
 			return NSD_ERR_FORMAT;
-		n = ext_table[slot].nlayers;
-		ids = ext_table[slot].id;
-		offs = ext_table[slot].off;
+		n = NSD_EXT_NLAYERS(ext_pool, slot);
+		if (n > NSD_EXT_MAX_LAYERS)
+			return NSD_ERR_FORMAT;
+		for (uint32_t k = 0; k < n; k++) {
+			ids[k] = (uint8_t)NSD_EXT_ID(ext_pool, slot, k);
+			offs[k] = (uint16_t)NSD_EXT_OFF(ext_pool, slot, k);
+		}
 	} else {
 		for (uint32_t k = 0; k < n; k++) {
-			lid[k] = (uint8_t)((rec.chain >> (5 * k)) & 31);
-			loff[k] = k ? (uint16_t)(rec.off2[k - 1] * 2u) : 0;
+			ids[k] = (uint8_t)((rec.chain >> (5 * k)) & 31);
+			offs[k] = k ? (uint16_t)(rec.off2[k - 1] * 2u) : 0;
 		}
-		ids = lid;
-		offs = loff;
 	}
 	const bool host = rec.nflags & NSD_F_HOST;
 	if (n == 0 && is_lt(linktype, NSD_LINKTYPE_EN10MB))
 		return NSD_ERR_FORMAT;
 
-	uint32_t tail = caplen;
+	uint32_t tail = caplen, data = rec.data_off;
 	for (uint32_t k = 0; k < n; k++) {
 		Layer L{ ids[k], offs[k], tail };
 		if (L.start > tail)
@@ -995,30 +997,40 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 		case NSD_OPS_UDP:            dn = r_udp(o, f, L, mode); break;
 		case NSD_OPS_ICMPV4:         dn = r_icmp(o, f, L, mode, rec.nflags & NSD_F_ICMP_BAD); break;
 		case NSD_OPS_ICMPV6:         dn = r_icmpv6(o, f, L, mode); break;
+		// leaves the device classifies and the host renders (NSD_F_HOST)
+		case NSD_OPS_ARP:            dn = r_arp(o, f, L, mode); break;
+		case NSD_OPS_LLDP:           dn = r_lldp(o, f, L, mode); break;
+		case NSD_OPS_IGMP:           dn = r_igmp(o, f, L, mode); break;
+		case NSD_OPS_DCCP:           dn = r_dccp(o, f, L, mode); break;
 		default:
-			dn = { L.start, L.tail, false, false };   // ARP, LLDP, IGMP, DCCP, SLL...
+			dn = { L.start, L.tail, false, false };   // SLL, 802.11, netlink heads
 		}
 		if (!dn.ok)
-			return (host && k + 1 == n) ? NSD_ERR_FORMAT : NSD_ERR_FORMAT;
+			return NSD_ERR_FORMAT;   // a body no host renderer covers yet (ICMPv6 130-154)
 		// consistency with the record: next layer's start / final cursor
 		if (k + 1 < n) {
 			if (!dn.next || dn.data != offs[k + 1])
+				return NSD_ERR_FORMAT;
+		} else if (host) {
+			// a host-rendered leaf: the device left the cursor at its start
+			if (dn.next || L.start != rec.data_off || dn.tail != rec.tail_off)
 				return NSD_ERR_FORMAT;
 		} else {
 			if (dn.next || dn.data != rec.data_off || dn.tail != rec.tail_off)
 				return NSD_ERR_FORMAT;
 		}
 		tail = dn.tail;
+		data = dn.data;
 	}
-	if (host)
+	if (host && n == 0)
 		return NSD_ERR_FORMAT;
 
-	// exit op (dissector.c:60-61)
+	// exit op (dissector.c:60-61) over what the last layer left
 	if (mode == PRINT_NORM) {
-		const uint32_t len = rec.tail_off - rec.data_off;
+		const uint32_t len = rec.tail_off - data;
 		if (len) {
-			dump_ascii(o, f, rec.data_off, len);
-			dump_hex(o, f, rec.data_off, len);
+			dump_ascii(o, f, data, len);
+			dump_hex(o, f, data, len);
 		}
 	}
 	o << "\n";
@@ -1045,7 +1057,7 @@ void format_post_dump(std::string &s, const uint8_t *pkt, uint32_t caplen, int m
 } // namespace nsd
 
 extern "C" long nsd_format_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-				  const nsd_rec *rec, const nsd_ext *ext_table, char *out, size_t cap)
+				  const nsd_rec *rec, const uint32_t *ext_pool, char *out, size_t cap)
 {
 	if (!pkt && caplen)
 		return NSD_ERR_ARG;
@@ -1053,7 +1065,7 @@ extern "C" long nsd_format_packet(const uint8_t *pkt, uint32_t caplen, int linkt
 		return NSD_ERR_ARG;
 	std::string s;
 	s.reserve(256 + 6 * (size_t)caplen);
-	int rc = nsd::format_packet(s, pkt, caplen, linktype, mode, *rec, ext_table);
+	int rc = nsd::format_packet(s, pkt, caplen, linktype, mode, *rec, ext_pool);
 	if (out && cap) {
 		size_t k = s.size() < cap - 1 ? s.size() : cap - 1;
 		memcpy(out, s.data(), k);
@@ -1068,7 +1080,7 @@ extern "C" long nsd_format_packet(const uint8_t *pkt, uint32_t caplen, int linkt
 // offsets in ends[] (so callers can split), status per packet in rc[] (may be
 // NULL).  Returns total bytes, or -needed when cap is too small.
 extern "C" long nsd_format_batch(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
-				 int linktype, int mode, const nsd_rec *rec, const nsd_ext *ext_table,
+				 int linktype, int mode, const nsd_rec *rec, const uint32_t *ext_pool,
 				 char *out, size_t cap, uint64_t *ends, int8_t *rc)
 {
 	std::string s;
@@ -1076,7 +1088,7 @@ extern "C" long nsd_format_batch(const uint8_t *frames, const nsd_desc_t *desc, 
 	for (uint32_t i = 0; i < n; i++) {
 		const uint64_t d = desc[i];
 		int r = nsd::format_packet(s, frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), linktype,
-					   mode, rec[i], ext_table);
+					   mode, rec[i], ext_pool);
 		if (rc)
 			rc[i] = (int8_t)r;
 		if (ends)

@@ -20,14 +20,14 @@
 #include "../../include/netsniff_dissect.h"
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
-				  int start_id, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+				  int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
 				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
 				  void *d_ws, int grid, hipStream_t stream);
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
 
 namespace nsd {
 int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-		  const nsd_rec &rec, const nsd_ext *ext_table);
+		  const nsd_rec &rec, const uint32_t *ext_pool);
 void format_post_dump(std::string &s, const uint8_t *pkt, uint32_t caplen, int mode, uint32_t from,
 		      uint32_t to);
 }
@@ -82,7 +82,7 @@ struct DevCtx {
 	uint8_t *frames = nullptr; size_t frames_cap = 0;
 	uint64_t *desc = nullptr; size_t desc_cap = 0;
 	nsd_rec *rec = nullptr; size_t rec_cap = 0;
-	nsd_ext *ext = nullptr; size_t ext_cap = 0;
+	uint32_t *ext = nullptr; size_t ext_cap = 0;   // ext pool (words)
 	uint32_t *ext_count = nullptr;
 	uint64_t *counters = nullptr;
 	uint8_t *ws = nullptr; size_t ws_cap = 0;          // queue for entry_batch
@@ -157,7 +157,7 @@ int start_for(int linktype) { return nsd_start_for(linktype); }
 extern "C" size_t nsd_workspace_bytes(uint32_t n) { return nsd_launch_workspace_bytes(n); }
 
 static int check_device_args(const uint8_t *d_frames, const nsd_desc_t *d_desc, const nsd_rec *d_rec,
-			     const nsd_ext *d_ext, uint32_t ext_cap, const uint32_t *d_ext_count,
+			     const uint32_t *d_ext, uint32_t ext_cap, const uint32_t *d_ext_count,
 			     const uint64_t *d_counters, int mode)
 {
 	if (!d_frames || !d_desc || !d_rec || !d_ext_count || !d_counters)
@@ -170,7 +170,7 @@ static int check_device_args(const uint8_t *d_frames, const nsd_desc_t *d_desc, 
 }
 
 extern "C" int nsd_dissect_device_ws(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
-				     int linktype, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+				     int linktype, int mode, nsd_rec *d_rec, uint32_t *d_ext,
 				     uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
 				     void *d_workspace, void *stream)
 {
@@ -187,7 +187,7 @@ extern "C" int nsd_dissect_device_ws(const uint8_t *d_frames, const nsd_desc_t *
 // grid override for experiments (0 = default)
 extern "C" int nsd_dissect_device_grid(const uint8_t *d_frames, const nsd_desc_t *d_desc,
 				       uint32_t n, int linktype, int mode, nsd_rec *d_rec,
-				       nsd_ext *d_ext, uint32_t ext_cap, uint32_t *d_ext_count,
+				       uint32_t *d_ext, uint32_t ext_cap, uint32_t *d_ext_count,
 				       uint64_t *d_counters, void *d_workspace, int grid, void *stream)
 {
 	if (n == 0)
@@ -203,7 +203,7 @@ extern "C" int nsd_dissect_device_grid(const uint8_t *d_frames, const nsd_desc_t
 // Without a caller workspace the library keeps one per process (allocated on
 // first use and grown on demand: that call is not graph-capturable).
 extern "C" int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_desc, uint32_t n,
-				  int linktype, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
+				  int linktype, int mode, nsd_rec *d_rec, uint32_t *d_ext,
 				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
 				  void *stream)
 {
@@ -223,7 +223,7 @@ extern "C" int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_d
 
 extern "C" int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
 				     const nsd_desc_t *desc, uint32_t n, int linktype, int mode,
-				     nsd_rec *rec, nsd_ext *ext, uint32_t ext_cap,
+				     nsd_rec *rec, uint32_t *ext, uint32_t ext_cap,
 				     uint32_t *ext_count, uint64_t *counters)
 {
 	if (n == 0)
@@ -263,7 +263,7 @@ extern "C" int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
 	if (ok && ext_cap) {
 		uint32_t k = used < ext_cap ? used : ext_cap;
 		if (k)
-			ok = hip_ok(hipMemcpy(ext, c.ext, k * sizeof(nsd_ext), hipMemcpyDeviceToHost), "D2H");
+			ok = hip_ok(hipMemcpy(ext, c.ext, (size_t)k * 4, hipMemcpyDeviceToHost), "D2H");
 	}
 	if (ext_count)
 		*ext_count = used;
@@ -379,22 +379,23 @@ extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype,
 	const int pm = parse_mode();
 	nsd_desc_t d = NSD_DESC(0, len);
 	nsd_rec rec;
-	nsd_ext ext;
+	uint32_t ext[NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS)];
 	uint32_t used = 0;
-	int rc = dissector_entry_batch(packet, len, &d, 1, linktype, pm, &rec, &ext, 1, &used, nullptr);
+	int rc = dissector_entry_batch(packet, len, &d, 1, linktype, pm, &rec, ext,
+				       NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS), &used, nullptr);
 	if (rc != NSD_OK) {
 		fprintf(stderr, "netsniff-dissect: device dissection failed (%d)\n", rc);
 		abort();   // like panic() (die.h:46): no CPU fallback
 	}
 	std::string s;
 	if (pm == PRINT_NORM || pm == PRINT_LESS) {
-		nsd::format_packet(s, packet, (uint32_t)len, linktype, pm, rec, &ext);
+		nsd::format_packet(s, packet, (uint32_t)len, linktype, pm, rec, ext);
 		// post-chain dumps run on what the chain left (dissector.c:108-118):
 		// after print_full the exit op already pulled everything
 		if (pm == PRINT_LESS)
 			nsd::format_post_dump(s, packet, (uint32_t)len, mode, rec.data_off, rec.tail_off);
 	} else {
-		nsd::format_packet(s, packet, (uint32_t)len, linktype, mode, rec, &ext);
+		nsd::format_packet(s, packet, (uint32_t)len, linktype, mode, rec, ext);
 	}
 	emit(s);
 }

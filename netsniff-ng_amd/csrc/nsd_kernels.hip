@@ -42,6 +42,9 @@ constexpr int row_of(int W) { return W / 4 + 1; }
 #ifndef NSD_CSUM_U
 #define NSD_CSUM_U 8               // interior chunk loads in flight per lane (dissect_icmp)
 #endif
+#ifndef NSD_MINW
+#define NSD_MINW 4                 // waves per SIMD the fused kernel is register-allocated for
+#endif
 #ifndef NSD_CSUM_SPLIT
 #define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
 #endif
@@ -397,8 +400,10 @@ struct Shared {
 	uint32_t step[64];                          // c_step, c_lay2h (general walk)
 	uint32_t qn;                                // pass-1 deferrals queued
 	uint32_t pn;                                // pass-2 pending checksums
-	uint32_t en, ebase;                         // ext scratch entries, their global base
+	uint32_t wc[WAVES][2];                      // per-wave ext pool chunk {next word, words left}
 	uint32_t pcnt[WAVES];                       // pass-1 pending checksums per wave
+	uint32_t q2;                                // pass-2 queue entries taken
+	uint32_t lay[WAVES][NSD_LDS_LAYERS * 64];   // pass-2 layer lists (layers 6..15)
 };
 
 // ---- pass 1 ------------------------------------------------------------------
@@ -409,7 +414,7 @@ struct Shared {
 template <int MODE>
 __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ frames,
 				      const uint64_t *__restrict__ desc, uint32_t n, int start_id,
-				      uint4 *__restrict__ rec, uint32_t *__restrict__ queue, uint32_t region,
+				      uint4 *__restrict__ rec, uint4 *__restrict__ queue, uint32_t region,
 				      uint64_t *__restrict__ pend)
 {
 	constexpr int ROW = row_of(WIN1);
@@ -421,7 +426,7 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 	const int wv = threadIdx.x >> 6;
 
 	const uint32_t stride = gridDim.x * BLOCK;
-	uint32_t *const bq = queue + (size_t)blockIdx.x * region;   // this block's queue region
+	uint4 *const bq = queue + (size_t)blockIdx.x * region;   // this block's queue region
 	// this wave's pending-checksum list (a wave visits region / WAVES packets)
 	uint64_t *const wq = pend + ((size_t)blockIdx.x * WAVES + wv) * (region / WAVES);
 	uint32_t npend = 0;
@@ -467,16 +472,17 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 
 		WalkOut w;
 		walk_init(w, caplen, valid ? start_id : 0);
-		bool deferred = false;
+		uint32_t fw = FW_DONE;
 		if (valid) {
 			const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
 					      (uint32_t)off & 15, 0, false };
 #ifdef NSD_X_NOWALK
 			w.chain = src.dw(3) & 0x3FF; w.n = 2; w.data = 42;
 #else
-			deferred = fast_walk<MODE>(src, caplen, w);
+			fw = fast_walk<MODE>(src, caplen, w);
 #endif
 		}
+		const bool deferred = fw != FW_DONE;
 		wave_sync_lds();
 		if (MODE == PRINT_NORM) {
 			// ICMPv4 messages past the window: listed for the checksum pass, which
@@ -495,8 +501,16 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 			if (lane == leader)
 				qb = atomicAdd(&s_qn, (uint32_t)__popcll(dm));   // LDS: no global contention
 			qb = __shfl(qb, leader, 64);
+			// queue entry: the packet, and where pass 2 resumes its walk
+			// (cursor, tail, layers so far, next ops, IPv4 checksum) or 0
+			// for a walk from the start
 			if (deferred)
-				bq[qb + lanes_below(dm)] = i;
+				bq[qb + lanes_below(dm)] =
+					fw == FW_RESUME
+						? make_uint4(i, w.data | w.tail << 16,
+							     (w.chain & 0xFFFFF) | (uint32_t)w.id << 20 | w.n << 25 | 1u << 31,
+							     w.ip_csum)
+						: make_uint4(i, 0, 0, 0);
 		}
 		const bool done = valid && !deferred;
 		// per-ops counts from the finished chains, grouped by chain word
@@ -531,160 +545,174 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 	fc.flush(s_cnt, lane);
 }
 
-// Block end of pass 2: the block's scratch ext entries move to the caller's
-// table at a range taken with one global atomic (so the table stays compact:
-// entries [0, min(count, cap)) are filled), and each owner record gets its
-// final slot (bytes 10..15: nflags, slot).  Entries past the capacity leave
-// their record with NSD_F_OVERFLOW and slot 0xFFFFFFFF.  16 lanes per entry,
-// lane t converting layers 4t .. 4t+3 (packed u32 -> id bytes + offsets);
-// entries past nlayers are not written.
-__device__ __forceinline__ void ext_compact(const ExtScr *scr, uint32_t &s_en, uint32_t &s_ebase,
-					    uint4 *rec, nsd_ext *ext, uint32_t ext_cap,
-					    uint32_t *ext_count, unsigned long long *counters)
-{
-	__syncthreads();
-	if (threadIdx.x == 0)
-		s_ebase = s_en ? atomicAdd(ext_count, s_en) : 0u;
-	__syncthreads();
-	const uint32_t ne = s_en, base = s_ebase;
-	const uint32_t t = threadIdx.x & 15;
-	uint32_t ovf = 0;
-	for (uint32_t j = threadIdx.x >> 4; j < ne; j += BLOCK / 16) {
-		const ExtScr *src = scr + j;
-		const uint32_t pkt = src->pkt, hdr = src->hdr;
-		const uint32_t nl = hdr & 0xFFFF, nf = hdr >> 16;
-		const uint32_t slot = base + j;
-		const bool fits = slot < ext_cap;
-		if (fits) {
-			uint8_t *dst = (uint8_t *)(ext + slot);
-			if (t == 0) {
-				*(uint32_t *)dst = pkt;
-				*(uint32_t *)(dst + 4) = nl;   // nlayers, rsvd 0
-			}
-			if (4 * t < nl) {
-				const uint4 l = *(const uint4 *)&src->lay[4 * t];
-				const uint32_t x[4] = { l.x, l.y, l.z, l.w };
-				uint32_t ids = 0, o01 = 0, o23 = 0;
-#pragma unroll
-				for (uint32_t u = 0; u < 4; u++) {
-					const uint32_t v = 4 * t + u < nl ? x[u] : 0u;
-					ids |= (v & 0xFF) << (8 * u);
-					if (u < 2)
-						o01 |= (v >> 16) << (16 * u);
-					else
-						o23 |= (v >> 16) << (16 * (u - 2));
-				}
-				*(uint32_t *)(dst + offsetof(nsd_ext, id) + 4 * t) = ids;
-				*(uint2 *)(dst + offsetof(nsd_ext, off) + 8 * t) = make_uint2(o01, o23);
-			}
-		}
-		if (t == 0) {
-			const uint32_t s = fits ? slot : 0xFFFFFFFFu;
-			const uint32_t f = fits ? nf : nf | NSD_F_OVERFLOW;
-			uint8_t *r = (uint8_t *)(rec + pkt);
-			*(uint16_t *)(r + 10) = (uint16_t)((f & 0xFF) | (s & 0xFF) << 8);
-			*(uint32_t *)(r + 12) = s >> 8;
-			ovf += !fits && !(nf & NSD_F_OVERFLOW);
-		}
-	}
-	if (t == 0 && ovf)
-		atomicAdd(&counters[NSD_CNT_OVERFLOW], (unsigned long long)ovf);
-}
-
-// ---- pass 2 ------------------------------------------------------------------
-// The packets pass 1 queued (the block's own queue region), walked from
-// scratch with the resumable general walk; ICMPv4 messages past the window go
-// to the block's pass-2 pending list (s_pn entries), ext chains to the
-// block's scratch (s_en entries, compacted by ext_compact).
+// The packets pass 1 queued (the block's own queue region), walked with the
+// resumable general walk.  Lanes are refilled: a lane whose chain ends takes
+// the next queued packet (entry and descriptor prefetched two rounds ahead),
+// so every round stages 64 useful windows instead of waiting for the wave's
+// slowest chain.  A round: stage each lane's 64-byte window at its cursor,
+// run layers until every lane has ended its chain or needs bytes past its
+// window, emit the ended ones.  ICMPv4 messages past the window go to the
+// block's pass-2 pending list (sh.pn entries), ext chains to the ext pool.
 template <int MODE>
 __device__ __forceinline__ void pass2(Shared &sh, const uint8_t *__restrict__ frames,
 				      const uint64_t *__restrict__ desc, int start_id, uint4 *__restrict__ rec,
-				      const uint32_t *__restrict__ queue, uint32_t region,
-				      uint64_t *__restrict__ pend2, ExtScr *__restrict__ scratch)
+				      const uint4 *__restrict__ queue, uint32_t region,
+				      uint64_t *__restrict__ pend2, uint32_t *__restrict__ ext, uint32_t ext_words,
+				      uint32_t *__restrict__ ext_used, uint32_t chunk)
 {
 	constexpr int ROW = row_of(WIN2);
-	auto &s_win = sh.win;
-	auto &s_pn = sh.pn;
-	unsigned long long *const s_cnt = sh.cnt;
-	const uint8_t *const s_lay3 = sh.lay3;
-	const uint32_t *const s_step = sh.step;
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
 	uint64_t *const bp = pend2 + (size_t)blockIdx.x * region;   // this block's pending list
-
 	const uint32_t nq = sh.qn;
-	const uint32_t *const bq = queue + (size_t)blockIdx.x * region;
-	ExtScr *const scr = scratch + (size_t)blockIdx.x * region;   // this block's ext scratch
-	const GenSink g{ scr, &sh.en, s_cnt };
+	const uint4 *const bq = queue + (size_t)blockIdx.x * region;
+	uint32_t *const lay = &sh.lay[wv][0];
+	const GenSink g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, lay };
 	FlagCnt fc;
 
-	for (uint32_t base = wv * 64; base < nq; base += BLOCK) {
-		const uint32_t k = base + lane;
-		const bool valid = k < nq;
-		const uint32_t i = valid ? bq[k] : 0;
-		const uint64_t d = valid ? desc[i] : 0;
-		const uint64_t off = NSD_DESC_OFF(d);
-		const uint32_t caplen = NSD_DESC_CAPLEN(d);
-		const uint32_t m = (uint32_t)off & 15;
+	bool have = false;            // the lane is walking a packet
+	WalkOut w;
+	walk_init(w, 0, 0);
+	uint32_t i = 0, caplen = 0, m = 0, wb = 0;
+	uint64_t d = 0;
+	uint4 pe = make_uint4(0, 0, 0, 0);   // prefetched queue entry
+	uint64_t pd = 0;                      // its descriptor
+	bool pa = false, pb = false;          // entry in flight / entry + descriptor in flight
+	bool drained = nq == 0;               // wave-uniform: no queue entries left to take
 
-		WalkOut w;
-		walk_init(w, caplen, valid ? start_id : 0);
-		uint32_t wb = 0;
-		bool part = valid;
-		// lanes whose next header lies past their window suspend; the wave
-		// restages those windows at the lanes' cursors and resumes them
-		for (;;) {
-			Chunks<WIN2> ch;
-			const uint32_t wbp = wb | (part ? 0u : 0x80000000u);
-			stage_load<true, WIN2>(ch, frames, d, wbp, lane);
-			stage_write(&s_win[wv][0], ch, lane);
-			wave_sync_lds();
-			const LSrc<false, WIN2> src{ &s_win[wv][lane * ROW], s_lay3, s_step, frames + off, caplen, m, wb,
-					       false };
-			bool susp;
-			for (;;) {
-				// a lane whose next layer would read past its window
-				// suspends for the rest of this round
-				const bool run = part && w.id != 0;
-				susp = run && src.near_end(w.data, w.id);
-				const bool act = run && !susp;
-				if (!__ballot(act))
-					break;
-				gen_step<MODE>(src, act, w, g);
+	for (;;) {
+		// (1) a lane without a packet takes its prefetched one
+		const bool take = !have && pb;
+		if (take) {
+			i = pe.x;
+			d = pd;
+			caplen = NSD_DESC_CAPLEN(d);
+			m = (uint32_t)NSD_DESC_OFF(d) & 15;
+			if (pe.z >> 31) {
+				// resume where pass 1 stopped: Ethernet, tags, IP recorded
+				walk_init(w, caplen, (int)((pe.z >> 20) & 31));
+				w.data = pe.y & 0xFFFF;
+				w.tail = pe.y >> 16;
+				w.chain = pe.z & 0xFFFFF;
+				w.n = (pe.z >> 25) & 7;
+				w.ip_csum = (uint16_t)pe.w;
+#pragma unroll
+				for (uint32_t k = 1; k < 4; k++)
+					if (k < w.n)   // layer k >= 1 of a fast-path chain starts at 14 + 4(k-1)
+						w.offA |= (uint64_t)(14 + 4 * (k - 1)) << (16 * k);
+#pragma unroll
+				for (uint32_t k = 0; k < 4; k++)
+					if (k < w.n)
+						atomicAdd(&sh.cnt[NSD_CNT_OPS + ((w.chain >> (5 * k)) & 31)], 1ull);
+			} else {
+				walk_init(w, caplen, start_id);
 			}
-			wave_sync_lds();
-			if (!__ballot(susp))
-				break;
-			part = susp;
-			if (susp)
-				wb = (w.data + m) & ~15u;
+			wb = (w.data + m) & ~15u;
+			have = true;
+			pb = false;
 		}
+		// (2) an entry that arrived in an earlier round: fetch its descriptor
+		if (pa && !pb) {
+			pd = desc[pe.x];
+			pb = true;
+			pa = false;
+		}
+		// (3) a lane with nothing prefetched takes the next queue entry
+		const bool want = !pa && !pb && !drained;
+		const uint64_t wm = __ballot(want);
+		if (wm) {
+			const int leader = __ffsll((unsigned long long)wm) - 1;
+			const uint32_t cnt = (uint32_t)__popcll(wm);
+			uint32_t qb = 0;
+			if (lane == leader)
+				qb = atomicAdd(&sh.q2, cnt);
+			qb = __shfl(qb, leader, 64);
+			const uint32_t kq = qb + lanes_below(wm);
+			if (want && kq < nq) {
+				pe = bq[kq];
+				pa = true;
+			}
+			drained = qb + cnt >= nq;
+		}
+		if (!__ballot(have)) {
+			if (!__ballot(pa || pb))
+				break;
+			continue;
+		}
+		// (4) stage every walking lane's window at its cursor
+		Chunks<WIN2> ch;
+		stage_load<true, WIN2>(ch, frames, d, wb | (have ? 0u : 0x80000000u), lane);
+		stage_write(&sh.win[wv][0], ch, lane);
+		wave_sync_lds();
+		// (5) layers until each lane ends its chain or needs bytes past its window
+		const LSrc<false, WIN2> src{ &sh.win[wv][lane * ROW], sh.lay3, sh.step, frames + NSD_DESC_OFF(d),
+					     caplen, m, wb, false };
+		bool susp;
+		for (;;) {
+			const bool run = have && w.id != 0;
+			susp = run && src.near_end(w.data, w.id);
+			const bool act = run && !susp;
+			if (!__ballot(act))
+				break;
+			gen_step<MODE>(src, act, w, g);
+		}
+		wave_sync_lds();
+		// (6) emit the lanes whose chain ended
+		const bool fin = have && !susp;
 		if (MODE == PRINT_NORM) {
-			const uint64_t pm = __ballot(w.icmp_pend);
+			const bool pnd = fin && w.icmp_pend;
+			const uint64_t pm = __ballot(pnd);
 			if (pm) {
 				const int leader = __ffsll((unsigned long long)pm) - 1;
-				uint32_t pb = 0;
+				uint32_t pb0 = 0;
 				if (lane == leader)
-					pb = atomicAdd(&s_pn, (uint32_t)__popcll(pm));
-				pb = __shfl(pb, leader, 64);
-				if (w.icmp_pend)
-					bp[pb + lanes_below(pm)] = pend_entry(i, w.icmp_off, w.icmp_len);
+					pb0 = atomicAdd(&sh.pn, (uint32_t)__popcll(pm));
+				pb0 = __shfl(pb0, leader, 64);
+				if (pnd)
+					bp[pb0 + lanes_below(pm)] = pend_entry(i, w.icmp_off, w.icmp_len);
 			}
 		}
-		if (!valid)
-			continue;
-#ifndef NSD_X_NOEXT
-		if (w.ext_on) {
-			ExtScr *e = scr + w.slot;
-			e->pkt = i;
-			e->hdr = (w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS) |
-				 (uint32_t)(NSD_N_EXT | w.flags) << 16;   // the record's nflags, for ext_compact
-		}
+		// ext chains: a pool entry (unless a deep chain took one already):
+		// header, layers 0..5 from the record registers, 6..15 from the
+		// LDS list (deeper ones are in the entry already)
+		const bool ex = fin && w.need_ext;
+		if (__ballot(ex)) {
+			const bool tk = ex && !w.ext_on;
+			const uint32_t sb = ext_take(g, tk, NSD_EXT_WORDS(NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS));
+			if (tk) {
+				w.slot = sb;
+				w.ext_on = true;
+			}
+			if (ex && w.slot == 0xFFFFFFFFu)
+				w.flags |= NSD_F_OVERFLOW;   // the pool is full
+#ifndef NSD_X_NOEXTW
+			if (ex && w.slot != 0xFFFFFFFFu) {
+				uint32_t *e = ext + w.slot;
+				const uint32_t nl = w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS;
+				auto lv = [&](uint32_t j) -> uint32_t {
+					if (j < NSD_REC_MAX_LAYERS)
+						return ((w.chain >> (5 * j)) & 31) | (uint32_t)off_of(w, j) << 16;
+					return j < nl ? lay[(j - NSD_REC_MAX_LAYERS) * 64 + lane] : 0u;
+				};
+				*(uint4 *)e = make_uint4(i, nl, 0, 0);
+				*(uint4 *)(e + 4) = make_uint4(lv(0), lv(1), lv(2), lv(3));
+				if (nl > 4)
+					*(uint4 *)(e + 8) = make_uint4(lv(4), lv(5), lv(6), lv(7));
+				if (nl > 8)
+					*(uint4 *)(e + 12) = make_uint4(lv(8), lv(9), lv(10), lv(11));
+				if (nl > 12)
+					*(uint4 *)(e + 16) = make_uint4(lv(12), lv(13), lv(14), lv(15));
+			}
 #endif
-		store_rec(rec, i, pack_record(w));
-		fc.add(w, caplen, true);
+		}
+		if (fin)
+			store_rec(rec, i, pack_record(w));
+		fc.add(w, caplen, fin);
+		have = have && susp;
+		if (susp)
+			wb = (w.data + m) & ~15u;
 	}
-	fc.flush(s_cnt, lane);
+	fc.flush(sh.cnt, lane);
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
@@ -766,38 +794,37 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 }
 
 // One launch per batch.  Each block of the persistent grid runs, in order:
-// pass 1 over its grid-stride tiles, pass 2 over the packets it queued, the
-// ext compaction, and the ICMPv4 checksums it left pending.  Every later
-// phase reads only what the same block wrote (its queue region, pending lists
-// and scratch), so the phases need block barriers, not grid-wide ones, and a
-// block's pass 2 / checksum work overlaps other blocks' pass 1.
+// pass 1 over its grid-stride tiles, pass 2 over the packets it queued, and
+// the ICMPv4 checksums it left pending.  Every later phase reads only what
+// the same block wrote (its queue region and pending lists), so the phases
+// need block barriers, not grid-wide ones, and a block's pass 2 / checksum
+// work overlaps other blocks' pass 1.
 template <int MODE>
-__global__ __launch_bounds__(BLOCK, 5) void dissect_all(
+__global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
-	uint4 *__restrict__ rec, nsd_ext *__restrict__ ext, uint32_t ext_cap,
-	uint32_t *__restrict__ ext_count, unsigned long long *__restrict__ counters,
-	uint32_t *__restrict__ queue, uint32_t region, uint64_t *__restrict__ pend,
-	uint64_t *__restrict__ pend2, ExtScr *__restrict__ scratch)
+	uint4 *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
+	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
+	uint4 *__restrict__ queue, uint32_t region, uint64_t *__restrict__ pend,
+	uint64_t *__restrict__ pend2)
 {
 	__shared__ Shared sh;
 	if (threadIdx.x == 0) {
 		sh.qn = 0;
 		sh.pn = 0;
-		sh.en = 0;
+		sh.q2 = 0;
 	}
 	if (threadIdx.x < 64)
 		sh.step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h.e[threadIdx.x - 32];
+	if (threadIdx.x < 2 * WAVES)
+		sh.wc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
 	block_init(sh.cnt, sh.lay3);   // (its barrier orders the stores above too)
 
 	pass1<MODE>(sh, frames, desc, n, start_id, rec, queue, region, pend);
 	if (MODE == PRINT_NORM || MODE == PRINT_LESS) {
 		__syncthreads();   // the block's queue and sh.qn are complete
 #ifndef NSD_X_NOP2
-		pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, scratch);
-#endif
-#ifndef NSD_X_NOEXT
-		ext_compact(scratch + (size_t)blockIdx.x * region, sh.en, sh.ebase, rec, ext, ext_cap,
-			    ext_count, counters);   // (starts with a barrier)
+		pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, ext, ext_words, ext_used,
+			    chunk);
 #endif
 	}
 	if (MODE == PRINT_NORM) {
@@ -813,7 +840,7 @@ __global__ __launch_bounds__(BLOCK, 5) void dissect_all(
 
 // ---- launcher (C ABI, called by nsd_host.cpp / nsd_pipe.cpp) -----------------
 // A persistent grid of at most NSD_MAX_GRID blocks; block b owns queue
-// region b, pending lists b and ext scratch b (room for every packet it
+// region b and pending lists b (room for every packet it
 // visits).
 constexpr uint32_t NSD_MAX_GRID = 4096;
 
@@ -829,17 +856,16 @@ static size_t region_slots(uint32_t n)
 	return ((size_t)n + (size_t)NSD_MAX_GRID * nsd::BLOCK + 1) & ~(size_t)1;
 }
 
-// workspace: the deferral queue (u32 per slot), the pass-1 and pass-2
-// pending-checksum lists (u64 per slot), the per-block ext scratch (ExtScr
-// per slot, 16-byte aligned)
+// workspace: the deferral queue (uint4 per slot), the pass-1 and pass-2
+// pending-checksum lists (u64 per slot)
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
-	return 16 + (4 + 8 + 8 + sizeof(nsd::ExtScr)) * region_slots(n);
+	return (16 + 8 + 8) * region_slots(n);
 }
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
-				  int start_id, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
-				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+				  int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
+				  uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
 				  void *d_ws, int grid, hipStream_t stream)
 {
 	using namespace nsd;
@@ -874,13 +900,21 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	if (blocks > cap_blocks)
 		blocks = cap_blocks;
 	const uint32_t region = region_for(n, blocks);
-	uint32_t *queue = (uint32_t *)d_ws;
+	uint4 *queue = (uint4 *)d_ws;
 	uint64_t *pend = (uint64_t *)(queue + region_slots(n));
 	uint64_t *pend2 = pend + region_slots(n);
-	ExtScr *scratch = (ExtScr *)(((uintptr_t)(pend2 + region_slots(n)) + 15) & ~(uintptr_t)15);
+	// ext pool chunk per request: half the pool spread over the waves, so the
+	// unused chunk tails the waves keep at the end waste at most half of it
+	// (a pool of 2x the words the chains need never overflows), within
+	// [1 deep entry, 512 short entries]
+	if (ext_words > NSD_EXT_POOL_MAX_WORDS)
+		ext_words = NSD_EXT_POOL_MAX_WORDS;
+	const uint64_t per = (uint64_t)ext_words / (2ull * blocks * WAVES);
+	const uint32_t lo = NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS), hi = 512 * NSD_EXT_WORDS(16);
+	const uint32_t chunk = (uint32_t)(per < lo ? lo : per > hi ? hi : per) & ~3u;
 	hipLaunchKernelGGL(mi == 0 ? dissect_all<PRINT_NORM> : mi == 1 ? dissect_all<PRINT_LESS> : dissect_all<PRINT_HEX>,
 			   dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id,
-			   (uint4 *)d_rec, d_ext, ext_cap, d_ext_count, (unsigned long long *)d_counters,
-			   queue, region, pend, pend2, scratch);
+			   (uint4 *)d_rec, d_ext, ext_words, d_ext_used, chunk, (unsigned long long *)d_counters,
+			   queue, region, pend, pend2);
 	return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -12,8 +12,8 @@
 #include "../../include/netsniff_dissect.h"
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
-				  int start_id, int mode, nsd_rec *d_rec, nsd_ext *d_ext,
-				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
+				  int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
+				  uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
 				  void *d_ws, int grid, hipStream_t stream);
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
 int nsd_start_for(int linktype);
@@ -36,7 +36,7 @@ struct Slot {
 	uint8_t *frames = nullptr;
 	uint64_t *desc = nullptr;
 	nsd_rec *rec = nullptr;
-	nsd_ext *ext = nullptr;
+	uint32_t *ext = nullptr;
 	uint32_t *small = nullptr;   // ext_count at +0, counters at +64 (device)
 	uint64_t *small_h = nullptr; // pinned host copy of the same 576 bytes
 	void *ws = nullptr;
@@ -44,7 +44,7 @@ struct Slot {
 	bool busy = false;
 	int status = NSD_OK;
 	uint32_t n = 0;
-	nsd_ext *ext_out = nullptr;
+	uint32_t *ext_out = nullptr;
 	uint32_t *ext_count_out = nullptr;
 	uint64_t *counters_out = nullptr;
 	int *status_out = nullptr;
@@ -54,7 +54,7 @@ struct Slot {
 struct nsd_pipe {
 	uint32_t max_pkts = 0;
 	size_t max_bytes = 0;
-	uint32_t ext_cap = 0;
+	uint32_t ext_cap = 0;   // ext pool words per batch
 	int depth = 0;
 	int start_id = 0;
 	int mode = 0;
@@ -110,7 +110,7 @@ extern "C" nsd_pipe *nsd_pipe_create(uint32_t max_pkts, size_t max_frame_bytes, 
 			    ok(hipMalloc(&s.frames, max_frame_bytes + NSD_FRAME_PAD), "hipMalloc") &&
 			    ok(hipMalloc(&s.desc, (size_t)max_pkts * 8), "hipMalloc") &&
 			    ok(hipMalloc(&s.rec, (size_t)max_pkts * sizeof(nsd_rec)), "hipMalloc") &&
-			    (!ext_cap || ok(hipMalloc(&s.ext, (size_t)ext_cap * sizeof(nsd_ext)), "hipMalloc")) &&
+			    (!ext_cap || ok(hipMalloc(&s.ext, (size_t)ext_cap * 4), "hipMalloc")) &&
 			    ok(hipMalloc(&s.small, 64 + NSD_NCOUNTERS * 8), "hipMalloc") &&
 			    ok(hipHostMalloc(&s.small_h, 64 + NSD_NCOUNTERS * 8, hipHostMallocDefault), "hipHostMalloc") &&
 			    ok(hipMalloc(&s.ws, nsd_launch_workspace_bytes(max_pkts)), "hipMalloc");
@@ -137,7 +137,7 @@ static int complete_oldest(nsd_pipe *p)
 			*s.ext_count_out = used;
 		const uint32_t k = used < p->ext_cap ? used : p->ext_cap;
 		if (k && s.ext_out &&
-		    !ok(hipMemcpyAsync(s.ext_out, s.ext, (size_t)k * sizeof(nsd_ext), hipMemcpyDeviceToHost,
+		    !ok(hipMemcpyAsync(s.ext_out, s.ext, (size_t)k * 4, hipMemcpyDeviceToHost,
 				       s.stream), "ext D2H"))
 			st = NSD_ERR_HIP;
 		if (k && s.ext_out && st == NSD_OK && !ok(hipStreamSynchronize(s.stream), "ext D2H"))
@@ -174,7 +174,7 @@ extern "C" int nsd_pipe_drain(nsd_pipe *p)
 }
 
 extern "C" int nsd_pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
-			       const nsd_desc_t *desc, uint32_t n, nsd_rec *rec, nsd_ext *ext,
+			       const nsd_desc_t *desc, uint32_t n, nsd_rec *rec, uint32_t *ext,
 			       uint32_t *ext_count, uint64_t *counters, int *status)
 {
 	if (!p || (n && (!frames || !desc || !rec)) || (p->ext_cap && !ext && n))

@@ -69,22 +69,59 @@ struct WalkOut {
 	uint32_t icmp_off, icmp_len;
 };
 
-// Pass 2's ext scratch entry (block-local, see ext_compact in
-// nsd_kernels.hip): one packed u32 per layer (ops id | start offset << 16),
-// so recording a layer is one store.
-struct ExtScr {
-	uint32_t pkt;
-	uint32_t hdr;                        // nlayers | record nflags << 16
-	uint32_t pad[2];                     // lay[] 16-byte aligned (ext_compact reads uint4)
-	uint32_t lay[NSD_EXT_MAX_LAYERS];
+// Where the general walk puts what it records beyond the 16-byte record:
+// layers 6 .. 6+NSD_LDS_LAYERS-1 in a per-lane LDS list (written out with the
+// packet's pool entry when its walk ends), deeper layers straight into the
+// packet's pool entry (taken when the chain reaches that depth).  Pool words
+// come from per-wave chunks (ext_take).
+#define NSD_LDS_LAYERS 10
+struct GenSink {
+	uint32_t *pool;               // the ext pool
+	uint32_t pool_words;
+	uint32_t *used;               // pool words handed out (global)
+	uint32_t chunk;               // words per chunk request
+	uint32_t *wc;                 // LDS: this wave's chunk {next word, words left}
+	unsigned long long *s_cnt;    // LDS: block counters
+	uint32_t *lay;                // LDS: this wave's layer lists, [j * 64 + lane]
 };
 
-// Where the general walk puts what it records beyond the 16-byte record.
-struct GenSink {
-	ExtScr *scr;                  // this block's scratch entries (room for every packet it walks)
-	uint32_t *s_n;                // LDS: scratch entries taken
-	unsigned long long *s_cnt;    // LDS: block counters
-};
+// Wave-uniform call: every lane with `want` gets a pool entry of `words`
+// words (consecutive lanes, consecutive entries) from the wave's chunk; a new
+// chunk is taken with one global atomic when the current one is short (its
+// tail is left unused).  Returns the entry's word index, or 0xFFFFFFFF when
+// it does not fit in the pool (or !want).
+__device__ __forceinline__ uint32_t ext_take(const GenSink &g, bool want, uint32_t words)
+{
+	const uint64_t m = __ballot(want);
+	if (!m)
+		return 0xFFFFFFFFu;
+	const int leader = __ffsll((unsigned long long)m) - 1;
+	const uint32_t need = (uint32_t)__popcll(m) * words;
+	uint32_t base = g.wc[0], left = g.wc[1];
+	if (left < need) {
+		// +3: the caller's running offset may not be a multiple of 4 (entries
+		// are written with 16-byte stores)
+		const uint32_t chunk = (g.chunk > need ? g.chunk : need) + 3;
+		uint32_t b = 0xFFFFFFFFu;
+		// a full pool takes no more chunks, so the counter cannot wrap round
+		// into it (the launcher caps pool_words well below 2^32)
+		if ((int)__lane_id() == leader &&
+		    __hip_atomic_load(g.used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g.pool_words)
+			b = atomicAdd(g.used, chunk);
+		b = __shfl(b, leader, 64);
+		if (b == 0xFFFFFFFFu)
+			return 0xFFFFFFFFu;   // the wave's chunk state stays empty
+		base = (b + 3) & ~3u;
+		left = chunk - (base - b);
+	}
+	if ((int)__lane_id() == leader) {
+		g.wc[0] = base + need;
+		g.wc[1] = left - need;
+	}
+	const uint32_t s = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+							 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0)) * words;
+	return want && (uint64_t)s + words <= g.pool_words ? s : 0xFFFFFFFFu;
+}
 
 __device__ __forceinline__ uint16_t off_of(const WalkOut &w, uint32_t k)
 {
@@ -200,7 +237,7 @@ __constant__ Lay2Hash c_lay2h;
 // bookkeeping, which made the scalar unit the bottleneck).  The rare heavy
 // bodies (IPv4 header checksum, ICMPv4 checksum, MPLS label walk) sit behind
 // wave-uniform branches.  `act`: the lane runs a layer in this call.  Per
-// layer: record the ops (chain word / offsets, or the ext scratch entry once
+// layer: record the ops (chain word / offsets, or the ext pool entry once
 // the chain needs the ext form), count it, advance the pkt_buff cursor
 // exactly as the reference parser does, look up the next ops.
 template <int MODE, class Src>
@@ -211,24 +248,13 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 	const uint32_t k = w.n;
 	// ---- record the layer: the first 6 in the record; more than 6, or a
 	// layer past byte 510, forces the ext form
+	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
 	const bool need_now = act && (k >= NSD_REC_MAX_LAYERS || (k >= 1 && start > 510));
-	const bool first = need_now && !w.ext_on;
-	const uint64_t fm = __ballot(first);
-	if (fm) {
-		const int leader = __ffsll((unsigned long long)fm) - 1;
-		uint32_t sb = 0;
-		if ((int)__lane_id() == leader)
-			sb = atomicAdd(g.s_n, (uint32_t)__popcll(fm));
-		sb = __shfl(sb, leader, 64);
-		sb += __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0));
-		if (first) {
-#ifndef NSD_X_NOEXT
-			ExtScr *e = g.scr + sb;
-#pragma unroll
-			for (uint32_t j = 0; j < NSD_REC_MAX_LAYERS; j++)
-				if (j < k)
-					e->lay[j] = ((w.chain >> (5 * j)) & 31) | (uint32_t)off_of(w, j) << 16;
-#endif
+	const bool deep_first = act && k == DEEP && !w.ext_on;
+	if (__ballot(deep_first)) {
+		// a chain this deep takes its pool entry now (rare)
+		const uint32_t sb = ext_take(g, deep_first, NSD_EXT_WORDS(DEEP + 1));
+		if (deep_first) {
 			w.slot = sb;
 			w.ext_on = true;
 		}
@@ -238,15 +264,16 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 	w.chain |= act && k < NSD_REC_MAX_LAYERS ? (uint32_t)id << (5 * kk) : 0u;
 	w.offA |= act && k < 4 ? (uint64_t)(start & 0xFFFF) << (16 * (kk & 3)) : 0ull;
 	w.offB |= act && k >= 4 && k < NSD_REC_MAX_LAYERS ? (start & 0xFFFF) << (16 * (kk & 1)) : 0u;
-	w.flags |= act && k >= NSD_EXT_MAX_LAYERS && w.ext_on ? NSD_F_OVERFLOW : 0;
+	w.flags |= act && k >= NSD_EXT_MAX_LAYERS ? NSD_F_OVERFLOW : 0;
 	if (act && k < NSD_EXT_MAX_LAYERS) {
 #ifndef NSD_X_NOCNT
 		atomicAdd(&g.s_cnt[NSD_CNT_OPS + id], 1ull);   // the oracle counts the first 64 layers
 #endif
-#ifndef NSD_X_NOEXT
-		if (w.ext_on)
-			g.scr[w.slot].lay[k] = (uint32_t)id | start << 16;
-#endif
+		const uint32_t lv = (uint32_t)id | start << 16;
+		if (k >= NSD_REC_MAX_LAYERS && k < DEEP)
+			g.lay[(k - NSD_REC_MAX_LAYERS) * 64 + __lane_id()] = lv;
+		else if (k >= DEEP && w.slot != 0xFFFFFFFFu)
+			g.pool[w.slot + NSD_EXT_HDR_WORDS + k] = lv;
 	}
 	w.n = act ? k + 1 : k;
 
@@ -363,12 +390,16 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 // Straight-line walk for the common chains (pass 1): Ethernet, up to two
 // 802.1Q / 802.1ad tags, IPv4 or IPv6, then TCP / UDP / ICMPv4 / ICMPv6 /
 // ESP / NoNext (or a host-rendered leaf: ARP, LLDP, IGMP, DCCP).  Same
-// semantics as walk() for every packet it finishes (the per-layer comments
-// there cite the reference); anything else (MPLS, deeper tag stacks,
-// extension headers, IPv6-in-IPv4, bytes past the staged window) returns true
-// and the packet goes to pass 2.  No loop, no per-layer dispatch switch.
+// semantics as gen_step() for every packet it finishes (the c_step table
+// cites the reference per ops); anything else (MPLS, deeper tag stacks,
+// extension headers, IPv6-in-IPv4, bytes past the staged window) goes to
+// pass 2.  No loop, no per-layer dispatch switch.
+// Returns FW_DONE, FW_RESTART (pass 2 walks the packet from its start) or
+// FW_RESUME (the chain reached an extension header / AH / IPv6-in-IPv4 ops
+// at w.data with layers 0..w.n-1 recorded: pass 2 resumes there with w.id).
+enum : uint32_t { FW_DONE = 0, FW_RESTART = 1, FW_RESUME = 2 };
 template <int MODE, class Src>
-__device__ __forceinline__ bool fast_walk(const Src &s, uint32_t caplen, WalkOut &w)
+__device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, WalkOut &w)
 {
 	uint32_t n = 0;
 	auto rec = [&](int id, uint32_t at) {
@@ -380,11 +411,11 @@ __device__ __forceinline__ bool fast_walk(const Src &s, uint32_t caplen, WalkOut
 		n++;
 	};
 	if (w.id != NSD_OPS_ETHERNET)
-		return true;   // other link types: pass 2
+		return FW_RESTART;   // other link types: pass 2
 	rec(NSD_OPS_ETHERNET, 0);
 	if (caplen < 14) {
 		w.n = n;
-		return false;
+		return FW_DONE;
 	}
 	uint32_t d = 14;
 	int next = lay2(s.be16(12));
@@ -396,7 +427,7 @@ __device__ __forceinline__ bool fast_walk(const Src &s, uint32_t caplen, WalkOut
 		if (caplen - d < 4) {
 			w.data = d;
 			w.n = n;
-			return s.missed();
+			return s.missed() ? FW_RESTART : FW_DONE;
 		}
 		next = lay2(s.be16(d + 2));
 		d += 4;
@@ -408,13 +439,13 @@ __device__ __forceinline__ bool fast_walk(const Src &s, uint32_t caplen, WalkOut
 		rec(NSD_OPS_IPV4, d);
 		if (caplen - d < 20) {
 			w.n = n;
-			return s.missed();
+			return s.missed() ? FW_RESTART : FW_DONE;
 		}
 		const uint32_t ihl = s.b(d) & 0xF;
 		const uint32_t proto = s.b(d + 9);
 		if (MODE == PRINT_NORM) {
 			if (!s.in_window(d, ihl * 4u))
-				return true;
+				return FW_RESTART;
 			w.ip_csum = calc_csum(s, d, ihl * 2u);
 		}
 		d2 = d + 20;
@@ -431,7 +462,7 @@ __device__ __forceinline__ bool fast_walk(const Src &s, uint32_t caplen, WalkOut
 		rec(NSD_OPS_IPV6, d);
 		if (caplen - d < 40) {
 			w.n = n;
-			return s.missed();
+			return s.missed() ? FW_RESTART : FW_DONE;
 		}
 		d2 = d + 40;
 		l4 = s.lay3(s.b(d + 6));
@@ -439,12 +470,12 @@ __device__ __forceinline__ bool fast_walk(const Src &s, uint32_t caplen, WalkOut
 		rec(next, d);
 		w.flags |= NSD_F_HOST;
 		w.n = n;
-		return s.missed();
+		return s.missed() ? FW_RESTART : FW_DONE;
 	} else if (next == 0) {
 		w.n = n;
-		return s.missed();
+		return s.missed() ? FW_RESTART : FW_DONE;
 	} else {
-		return true;   // MPLS, a third tag
+		return FW_RESTART;   // MPLS, a third tag
 	}
 	w.data = d2;
 	const uint32_t len = w.tail - d2;
@@ -500,10 +531,15 @@ __device__ __forceinline__ bool fast_walk(const Src &s, uint32_t caplen, WalkOut
 		w.flags |= NSD_F_HOST;
 		break;
 	default:
-		return true;   // extension headers, AH, IPv6-in-IPv4
+		// extension headers, AH, IPv6-in-IPv4: pass 2 resumes at d2
+		if (s.missed())
+			return FW_RESTART;
+		w.n = n;
+		w.id = l4;
+		return FW_RESUME;
 	}
 	w.n = n;
-	return s.missed();
+	return s.missed() ? FW_RESTART : FW_DONE;
 }
 
 } // namespace nsd

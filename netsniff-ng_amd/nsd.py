@@ -23,10 +23,35 @@ FRAME_PAD = 64
 
 REC_DTYPE = np.dtype([("chain", "<u4"), ("data_off", "<u2"), ("tail_off", "<u2"),
                       ("ip_csum", "<u2"), ("nflags", "u1"), ("off2", "u1", (5,))])
-EXT_DTYPE = np.dtype([("pkt", "<u4"), ("nlayers", "<u2"), ("rsvd", "<u2"),
-                      ("id", "u1", (64,)), ("off", "<u2", (64,))])
 REC_BYTES = 16
-EXT_BYTES = 200
+
+# ext pool (include/netsniff_dissect.h "ext pool"): u32 words; an entry is a
+# 4-word header {packet, nlayers, 0, 0} + one word per layer (id | off << 16)
+EXT_HDR_WORDS = 4
+EXT_MAX_LAYERS = 64
+
+# struct sock_filter (linux/filter.h) = nsd_bpf_insn
+BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])
+
+
+def ext_words(nlayers):
+    """Words one pool entry of a chain of `nlayers` layers occupies (NSD_EXT_WORDS)."""
+    return EXT_HDR_WORDS + (16 if nlayers <= 16 else EXT_MAX_LAYERS)
+
+
+def ext_pool_words(n):
+    """NSD_EXT_POOL_WORDS(n): a pool that never overflows for n packets whose
+    chains are at most 16 layers, plus room for a few deeper ones."""
+    return 48 * n + 4096
+
+
+def ext_entry(pool, slot):
+    """(packet, ids tuple, offsets tuple) of the pool entry at word `slot`."""
+    p = np.asarray(pool).view(np.uint32)
+    nl = int(p[slot + 1]) & 0xFFFF
+    words = p[slot + EXT_HDR_WORDS: slot + EXT_HDR_WORDS + nl]
+    return int(p[slot]), tuple(int(x) & 0xFF for x in words), tuple(int(x) >> 16 for x in words)
+
 
 OPS_NAMES = ["invalid", "ethernet", "vlan", "QinQ", "mpls_uc", "arp", "lldp", "ipv4", "ipv6",
              "ipv6_in_ipv4", "icmpv4", "icmpv6", "igmp", "ip_auth", "ip_esp", "ipv6_dest_opts",
@@ -36,10 +61,12 @@ OPS_NAMES = ["invalid", "ethernet", "vlan", "QinQ", "mpls_uc", "arp", "lldp", "i
 # every entry point declared in include/netsniff_dissect.h
 ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup_all",
                "dissector_set_print_type", "nsd_dissect_device", "dissector_entry_batch",
-               "nsd_workspace_bytes", "nsd_dissect_device_ws", "nsd_format_packet", "nsd_lookup_init", "nsd_lookup_cleanup", "nsd_tprintf_wrap",
-               "nsd_version", "nsd_device_count", "nsd_pipe_create", "nsd_pipe_submit",
-               "nsd_pipe_wait", "nsd_pipe_drain", "nsd_pipe_destroy", "nsd_host_alloc",
-               "nsd_host_free", "nsd_host_register", "nsd_host_unregister"]
+               "nsd_workspace_bytes", "nsd_dissect_device_ws", "nsd_format_packet", "nsd_lookup_init",
+               "nsd_lookup_cleanup", "nsd_tprintf_wrap", "nsd_version", "nsd_device_count",
+               "nsd_pipe_create", "nsd_pipe_submit", "nsd_pipe_wait", "nsd_pipe_drain",
+               "nsd_pipe_destroy", "nsd_host_alloc", "nsd_host_free", "nsd_host_register",
+               "nsd_host_unregister", "nsd_bpf_validate", "nsd_bpf_load", "nsd_bpf_free",
+               "nsd_bpf_workspace_bytes", "nsd_bpf_filter_device", "nsd_bpf_filter_batch"]
 
 _lib = None
 _vp, _u32, _u64, _int, _sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
@@ -103,6 +130,18 @@ def lib():
         L.nsd_host_unregister.argtypes = [_vp]
         L.dissector_init_all.argtypes = [_int]
         L.dissector_entry_point.argtypes = [_vp, _sz, _int, _int, _vp]
+        L.nsd_bpf_validate.restype = _int
+        L.nsd_bpf_validate.argtypes = [_vp, _u32]
+        L.nsd_bpf_load.restype = _vp
+        L.nsd_bpf_load.argtypes = [_vp, _u32]
+        L.nsd_bpf_free.restype = None
+        L.nsd_bpf_free.argtypes = [_vp]
+        L.nsd_bpf_workspace_bytes.restype = _sz
+        L.nsd_bpf_workspace_bytes.argtypes = [_u32]
+        L.nsd_bpf_filter_device.restype = _int
+        L.nsd_bpf_filter_device.argtypes = [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
+        L.nsd_bpf_filter_batch.restype = _int
+        L.nsd_bpf_filter_batch.argtypes = [_vp, _vp, _sz, _vp, _u32, _vp]
         _lib = L
     return _lib
 
@@ -117,23 +156,25 @@ def _check(rc, what):
 
 
 def dissect_device(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, rec=None, ext=None,
-                   ext_count=None, counters=None, grid=0, stream=None, workspace=None):
+                   ext_used=None, counters=None, grid=0, stream=None, workspace=None):
     """Walk a device-resident batch.  frames: uint8 cuda tensor (padded by
     FRAME_PAD bytes), desc: int64/uint64 cuda tensor (packed descriptors).
-    Returns (rec u8[n*16], ext u8[cap*200], ext_count i32[1], counters i64[64])
-    as cuda tensors; counters/ext_count accumulate if passed in."""
+    Returns (rec u8[n*16], ext i32[words] (the pool), ext_used i32[1] (pool
+    words handed out), counters i64[64]) as cuda tensors; counters and
+    ext_used accumulate if passed in."""
     import torch
     n = desc.numel()
     dev = desc.device
     if rec is None:
         rec = torch.empty(n * REC_BYTES, dtype=torch.uint8, device=dev)
     if ext is None:
-        ext = torch.empty(max(n, 1) * EXT_BYTES, dtype=torch.uint8, device=dev)
-    if ext_count is None:
-        ext_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        ext = torch.empty(ext_pool_words(n), dtype=torch.int32, device=dev)
+    if ext_used is None:
+        ext_used = torch.zeros(1, dtype=torch.int32, device=dev)
     if counters is None:
         counters = torch.zeros(NCOUNTERS, dtype=torch.int64, device=dev)
-    ext_cap = ext.numel() // EXT_BYTES
+    assert ext.element_size() == 4, "the ext pool is u32 words"
+    words = ext.numel()
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
     L = lib()
@@ -141,33 +182,33 @@ def dissect_device(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, rec=
         workspace = torch.empty(L.nsd_workspace_bytes(n), dtype=torch.uint8, device=dev)
     if grid:
         rc = L.nsd_dissect_device_grid(frames.data_ptr(), desc.data_ptr(), n, linktype, mode,
-                                       rec.data_ptr(), ext.data_ptr(), ext_cap, ext_count.data_ptr(),
+                                       rec.data_ptr(), ext.data_ptr(), words, ext_used.data_ptr(),
                                        counters.data_ptr(), workspace.data_ptr(), grid, stream)
     else:
         rc = L.nsd_dissect_device_ws(frames.data_ptr(), desc.data_ptr(), n, linktype, mode,
-                                     rec.data_ptr(), ext.data_ptr(), ext_cap, ext_count.data_ptr(),
+                                     rec.data_ptr(), ext.data_ptr(), words, ext_used.data_ptr(),
                                      counters.data_ptr(), workspace.data_ptr(), stream)
     _check(rc, "nsd_dissect_device")
-    return rec, ext, ext_count, counters
+    return rec, ext, ext_used, counters
 
 
-def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_cap=None):
+def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_words=None):
     """Host-memory batch through the device (H2D, kernel, D2H).
-    Returns (rec, ext[:count], counters) as numpy arrays."""
+    Returns (rec, ext pool words[:used], counters) as numpy arrays."""
     frames = np.ascontiguousarray(frames, dtype=np.uint8)
     desc = np.ascontiguousarray(desc, dtype=np.uint64)
     n = len(desc)
-    if ext_cap is None:
-        ext_cap = n
+    if ext_words is None:
+        ext_words = ext_pool_words(n)
     rec = np.zeros(n, dtype=REC_DTYPE)
-    ext = np.zeros(max(ext_cap, 1), dtype=EXT_DTYPE)
-    cnt = np.zeros(1, dtype=np.uint32)
+    ext = np.zeros(max(ext_words, 1), dtype=np.uint32)
+    used = np.zeros(1, dtype=np.uint32)
     counters = np.zeros(NCOUNTERS, dtype=np.uint64)
     rc = lib().dissector_entry_batch(frames.ctypes.data, frames.nbytes, desc.ctypes.data, n,
-                                     linktype, mode, rec.ctypes.data, ext.ctypes.data, ext_cap,
-                                     cnt.ctypes.data, counters.ctypes.data)
+                                     linktype, mode, rec.ctypes.data, ext.ctypes.data, ext_words,
+                                     used.ctypes.data, counters.ctypes.data)
     _check(rc, "dissector_entry_batch")
-    return rec, ext[:min(int(cnt[0]), ext_cap)], counters
+    return rec, ext[:min(int(used[0]), ext_words)], counters
 
 
 class Pipe:
@@ -175,24 +216,27 @@ class Pipe:
     land in the caller's arrays when the batch completes.  Arrays passed to
     submit() are kept alive until then."""
 
-    def __init__(self, max_pkts, max_frame_bytes, ext_cap=0, depth=3, mode=PRINT_NORM,
+    def __init__(self, max_pkts, max_frame_bytes, ext_words=0, depth=3, mode=PRINT_NORM,
                  linktype=LINKTYPE_EN10MB):
         self.L = lib()
-        self.p = self.L.nsd_pipe_create(max_pkts, max_frame_bytes, ext_cap, depth, linktype, mode)
+        self.p = self.L.nsd_pipe_create(max_pkts, max_frame_bytes, ext_words, depth, linktype, mode)
         if not self.p:
             raise NsdError("nsd_pipe_create failed")
-        self.ext_cap = ext_cap
+        self.ext_words = ext_words
         self.depth = depth
         self.inflight = []
 
-    def submit(self, frames, desc, rec, ext=None, ext_count=None, counters=None, status=None):
+    def submit(self, frames, desc, rec, ext=None, ext_used=None, counters=None, status=None):
+        """ext: u32[ext_words] receiving the pool, ext_used: u32[1]."""
         n = len(desc)
         ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+        if ext is not None:
+            assert ext.dtype == np.uint32 and len(ext) >= self.ext_words
         rc = self.L.nsd_pipe_submit(self.p, frames.ctypes.data, frames.nbytes, desc.ctypes.data, n,
-                                    rec.ctypes.data, ptr(ext), ptr(ext_count), ptr(counters),
+                                    rec.ctypes.data, ptr(ext), ptr(ext_used), ptr(counters),
                                     ptr(status))
         _check(rc, "nsd_pipe_submit")
-        self.inflight.append((frames, desc, rec, ext, ext_count, counters, status))
+        self.inflight.append((frames, desc, rec, ext, ext_used, counters, status))
         if len(self.inflight) > self.depth:   # the library completed the oldest first
             self.inflight.pop(0)
 
@@ -217,16 +261,14 @@ class Pipe:
 
 
 def format_batch(frames, desc, rec, ext=None, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB):
-    """Render records to the reference text.  Returns (list of bytes per
-    packet, status array)."""
+    """Render records to the reference text (ext: the u32 pool the records'
+    slots index).  Returns (list of bytes per packet, status array)."""
     n = len(desc)
     frames = np.ascontiguousarray(frames, dtype=np.uint8)
     desc = np.ascontiguousarray(desc, dtype=np.uint64)
     rec = np.ascontiguousarray(rec)
-    ext_ptr = None if ext is None or len(ext) == 0 else np.ascontiguousarray(ext).ctypes.data
-    ext_keep = None if ext is None else np.ascontiguousarray(ext)
-    if ext_keep is not None and len(ext_keep):
-        ext_ptr = ext_keep.ctypes.data
+    ext_keep = None if ext is None or len(ext) == 0 else np.ascontiguousarray(ext).view(np.uint32)
+    ext_ptr = None if ext_keep is None else ext_keep.ctypes.data
     ends = np.zeros(n, dtype=np.uint64)
     rc = np.zeros(n, dtype=np.int8)
     cap = int(frames.nbytes) * 7 + 1024 * n + 4096
@@ -272,3 +314,68 @@ def unpack_counters(counters):
                     ("overflow", CNT_OVERFLOW), ("trim", CNT_TRIM)]:
         out[name] = int(c[k])
     return out
+
+
+# ---- classic BPF (nsd_bpf_*: the capture loop's filter step) -------------------------
+def bpf_validate(prog):
+    """__bpf_validate (bpf.c:388-506) through the product library: 1 / 0."""
+    p = np.ascontiguousarray(prog, dtype=BPF_INSN)
+    return lib().nsd_bpf_validate(p.ctypes.data if len(p) else None, len(p))
+
+
+class BpfProgram:
+    """A classic-BPF program validated, decoded and loaded on the device
+    (nsd_bpf_load); raises NsdError for an invalid program or without a GPU."""
+
+    def __init__(self, prog):
+        self.L = lib()
+        p = np.ascontiguousarray(prog, dtype=BPF_INSN)
+        self.h = self.L.nsd_bpf_load(p.ctypes.data if len(p) else None, len(p))
+        if not self.h:
+            raise NsdError("nsd_bpf_load refused the program (invalid program or no GPU)")
+        self.len = len(p)
+
+    def filter_batch(self, frames, desc):
+        """Host-memory batch -> u32 verdict per packet (0 = drop)."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        desc = np.ascontiguousarray(desc, dtype=np.uint64)
+        v = np.zeros(len(desc), dtype=np.uint32)
+        rc = self.L.nsd_bpf_filter_batch(self.h, frames.ctypes.data, frames.nbytes, desc.ctypes.data,
+                                         len(desc), v.ctypes.data)
+        _check(rc, "nsd_bpf_filter_batch")
+        return v
+
+    def filter_device(self, frames, desc, compact=False, verdict=None, out=None, count=None,
+                      workspace=None, stream=None):
+        """Device-resident batch on torch's current stream.  Returns
+        (verdict i32[n], accepted descriptors i64[n] or None, count i32[1] or
+        None); with compact=True the accepted packets' descriptors are packed
+        in batch order into out[:count]."""
+        import torch
+        n = desc.numel()
+        dev = desc.device
+        if verdict is None:
+            verdict = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        if compact:
+            if out is None:
+                out = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+            if count is None:
+                count = torch.zeros(1, dtype=torch.int32, device=dev)
+            if workspace is None:
+                workspace = torch.empty(self.L.nsd_bpf_workspace_bytes(n), dtype=torch.uint8, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = self.L.nsd_bpf_filter_device(self.h, frames.data_ptr(), desc.data_ptr(), n, verdict.data_ptr(),
+                                          out.data_ptr() if compact else None,
+                                          count.data_ptr() if compact else None,
+                                          workspace.data_ptr() if compact else None, stream)
+        _check(rc, "nsd_bpf_filter_device")
+        return verdict[:n], out, count
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.nsd_bpf_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()

@@ -1489,8 +1489,8 @@ static void count(uint64_t *c, const nsd_rec *r, const nsor_info *in, uint32_t c
 }
 
 uint64_t nsor_dissect_batch(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
-			    int linktype, int mode, nsd_rec *rec, nsd_ext *ext,
-			    uint32_t ext_cap, uint32_t *ext_count, uint64_t *counters)
+			    int linktype, int mode, nsd_rec *rec, uint32_t *ext,
+			    uint32_t ext_words, uint32_t *ext_used, uint64_t *counters)
 {
 	uint64_t sw = 0;
 	nsor_info in;
@@ -1501,17 +1501,24 @@ uint64_t nsor_dissect_batch(const uint8_t *frames, const nsd_desc_t *desc, uint3
 		uint32_t caplen = NSD_DESC_CAPLEN(d);
 		nsor_dissect(frames + NSD_DESC_OFF(d), caplen, linktype, mode, NULL, &r, &in);
 		if ((r.nflags & 7) == NSD_N_EXT) {
-			uint32_t slot = ext_count ? (*ext_count)++ : UINT32_MAX;
-			if (ext && slot < ext_cap) {
-				nsd_ext *e = &ext[slot];
-				uint32_t m = in.nlayers < NSD_EXT_MAX_LAYERS ? in.nlayers : NSD_EXT_MAX_LAYERS;
-				memset(e, 0, sizeof(*e));
-				e->pkt = i;
-				e->nlayers = (uint16_t)m;
-				memcpy(e->id, in.id, m);
-				memcpy(e->off, in.off, m * sizeof(uint16_t));
+			/* dense pool entries in packet order (layout: netsniff_dissect.h) */
+			const uint32_t m = in.nlayers < NSD_EXT_MAX_LAYERS ? in.nlayers : NSD_EXT_MAX_LAYERS;
+			const uint32_t words = NSD_EXT_WORDS(m);
+			uint32_t slot = UINT32_MAX;
+			if (ext_used) {
+				const uint32_t at = *ext_used;
+				*ext_used += words;
+				if (ext && (uint64_t)at + words <= ext_words)
+					slot = at;
+			}
+			if (slot != UINT32_MAX) {
+				uint32_t *e = ext + slot;
+				memset(e, 0, words * sizeof(uint32_t));
+				e[0] = i;
+				e[1] = m;
+				for (uint32_t k = 0; k < m; k++)
+					e[NSD_EXT_HDR_WORDS + k] = in.id[k] | (uint32_t)in.off[k] << 16;
 			} else {
-				slot = UINT32_MAX;
 				r.nflags |= NSD_F_OVERFLOW;
 			}
 			memcpy(r.off2, &slot, 4);

@@ -50,12 +50,14 @@ typedef struct nsor_info {
 void nsor_dissect(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
 		  nsor_text *text, nsd_rec *rec, nsor_info *info);
 
-/* Batch form producing exactly what the device produces.  ext slots are
- * assigned in packet order (the device assigns them in arbitrary order; tests
- * compare through the slot indirection).  counters accumulate. Returns sum W. */
+/* Batch form producing exactly what the device produces.  Ext pool entries
+ * are packed densely in packet order (the device hands them out in
+ * arbitrary order from per-wave chunks; tests compare through the slot
+ * indirection).  *ext_used accumulates the words taken; counters
+ * accumulate.  Returns sum W. */
 uint64_t nsor_dissect_batch(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
-			    int linktype, int mode, nsd_rec *rec, nsd_ext *ext,
-			    uint32_t ext_cap, uint32_t *ext_count, uint64_t *counters);
+			    int linktype, int mode, nsd_rec *rec, uint32_t *ext,
+			    uint32_t ext_words, uint32_t *ext_used, uint64_t *counters);
 
 /* Same walk, text for every packet appended to *text (fields+text baseline). */
 uint64_t nsor_dissect_batch_text(const uint8_t *frames, const nsd_desc_t *desc,

@@ -54,9 +54,11 @@ def rec_digest(rec, ext):
             slot = int.from_bytes(bytes(r["off2"][:4]), "little")
             h.update(r.tobytes()[:11])
             if slot != 0xFFFFFFFF:
-                e = ext[slot]
-                m = int(e["nlayers"])
-                h.update(e["id"][:m].tobytes() + e["off"][:m].tobytes())
+                # pool entry: {pkt, nlayers, 0, 0, id | off << 16 ...}; hashed
+                # as u8 ids then LE u16 offsets
+                m = int(ext[slot + 1]) & 0xFFFF
+                w = np.asarray(ext[slot + 4:slot + 4 + m], dtype=np.uint32)
+                h.update((w & 0xFF).astype(np.uint8).tobytes() + (w >> 16).astype("<u2").tobytes())
         else:
             h.update(r.tobytes())
     return h.hexdigest()

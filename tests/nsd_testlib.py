@@ -23,9 +23,6 @@ SEED = 0x5EED
 REC_DTYPE = np.dtype([("chain", "<u4"), ("data_off", "<u2"), ("tail_off", "<u2"),
                       ("ip_csum", "<u2"), ("nflags", "u1"), ("off2", "u1", (5,))])
 assert REC_DTYPE.itemsize == 16
-EXT_DTYPE = np.dtype([("pkt", "<u4"), ("nlayers", "<u2"), ("rsvd", "<u2"),
-                      ("id", "u1", (64,)), ("off", "<u2", (64,))])
-assert EXT_DTYPE.itemsize == 200
 NCOUNTERS = 64
 
 
@@ -155,20 +152,20 @@ def oracle():
     return _oracle
 
 
-def oracle_records(frames, desc, linktype=1, mode=PRINT_NORM, ext_cap=None):
-    """Returns (rec, ext[:count], counters, sum_w)."""
+def oracle_records(frames, desc, linktype=1, mode=PRINT_NORM, ext_words=None):
+    """Returns (rec, ext pool words[:used], counters, sum_w)."""
     lib = oracle()
     n = len(desc)
-    if ext_cap is None:
-        ext_cap = n
+    if ext_words is None:
+        ext_words = 48 * n + 4096          # NSD_EXT_POOL_WORDS(n)
     rec = np.zeros(n, dtype=REC_DTYPE)
-    ext = np.zeros(max(ext_cap, 1), dtype=EXT_DTYPE)
-    cnt = np.zeros(1, dtype=np.uint32)
+    ext = np.zeros(max(ext_words, 1), dtype=np.uint32)
+    used = np.zeros(1, dtype=np.uint32)
     counters = np.zeros(NCOUNTERS, dtype=np.uint64)
     sw = lib.nsor_dissect_batch(frames.ctypes.data, desc.ctypes.data, n, linktype, mode,
-                                rec.ctypes.data, ext.ctypes.data, ext_cap, cnt.ctypes.data,
+                                rec.ctypes.data, ext.ctypes.data, ext_words, used.ctypes.data,
                                 counters.ctypes.data)
-    return rec, ext[:min(int(cnt[0]), ext_cap)], counters, int(sw)
+    return rec, ext[:min(int(used[0]), ext_words)], counters, int(sw)
 
 
 def oracle_text_packets(frames, desc, linktype=1, mode=PRINT_NORM):

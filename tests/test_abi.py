@@ -33,7 +33,8 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_record_layout_matches_header():
-    assert nsd.REC_DTYPE.itemsize == 16 and nsd.EXT_DTYPE.itemsize == 200
+    assert nsd.REC_DTYPE.itemsize == 16 and nsd.BPF_INSN.itemsize == 8
+    assert nsd.ext_words(6) == 20 and nsd.ext_words(16) == 20 and nsd.ext_words(17) == 68
     assert nsd.REC_DTYPE.fields["nflags"][1] == 10 and nsd.REC_DTYPE.fields["off2"][1] == 11
 
 

@@ -20,10 +20,9 @@ def _chain(rec, ext, i):
         slot = int.from_bytes(bytes(r["off2"][:4]), "little")
         if slot == 0xFFFFFFFF:
             return ("overflow",)
-        e = ext[slot]
-        m = int(e["nlayers"])
-        assert int(e["pkt"]) == i
-        return tuple(int(x) for x in e["id"][:m]), tuple(int(x) for x in e["off"][:m])
+        pkt, ids, offs = nsd.ext_entry(ext, slot)
+        assert pkt == i
+        return ids, offs
     ids = tuple((int(r["chain"]) >> (5 * k)) & 31 for k in range(n))
     offs = tuple([0] + [2 * int(x) for x in r["off2"][:max(n - 1, 0)]])
     return ids, offs[:n]
@@ -82,11 +81,11 @@ def test_device_resident_torch():
     frames, desc = T.make_batch(T.SYN_IMIX, 50000)
     f = torch.from_numpy(frames).cuda()
     d = torch.from_numpy(desc.view(np.int64)).cuda()
-    rec, ext, ext_count, counters = nsd.dissect_device(f, d, mode=T.PRINT_NORM)
+    rec, ext, ext_used, counters = nsd.dissect_device(f, d, mode=T.PRINT_NORM)
     torch.cuda.synchronize()
     drec = rec.cpu().numpy().view(nsd.REC_DTYPE)
     orec, oext, ocnt, _ = T.oracle_records(frames, desc)
-    dext = ext.cpu().numpy().view(nsd.EXT_DTYPE)[:int(ext_count.item())]
+    dext = ext.cpu().numpy().view(np.uint32)[:int(ext_used.item())]
     assert_same_records(drec, orec, dext, oext)
     assert np.array_equal(counters.cpu().numpy().view(np.uint64), ocnt)
 
@@ -98,24 +97,31 @@ def test_empty_batch_and_caplen_limit():
         nsd.entry_batch(np.zeros(70000, np.uint8), np.array([T.desc_pack(0, 66000)], np.uint64))
 
 
-def test_ext_table_full():
-    """A too-small ext table: exactly min(cap, needed) packets hold a slot,
-    each slot matches the oracle's chain for its packet, the rest carry
-    NSD_F_OVERFLOW with slot 0xFFFFFFFF."""
+@pytest.mark.parametrize("words", [0, 68, 200])
+def test_ext_pool_full(words):
+    """A pool too small for every ext chain: the packets holding an entry
+    match the oracle's chain, every entry lies inside the pool and no two
+    overlap, the rest carry NSD_F_OVERFLOW with slot 0xFFFFFFFF."""
     frames, desc = T.batch_from_packets(edge_cases.cases())
-    rec, ext, cnt = nsd.entry_batch(frames, desc, ext_cap=1)
+    rec, ext, cnt = nsd.entry_batch(frames, desc, ext_words=words)
     orec, oext, _, _ = T.oracle_records(frames, desc)          # full-capacity reference
     need = np.nonzero((orec["nflags"] & 7) == 7)[0]
+    assert len(need) > 2
     assert np.array_equal(np.nonzero((rec["nflags"] & 7) == 7)[0], need)
-    holders = 0
+    spans = []
     for i in need:
         slot = int.from_bytes(bytes(rec[i]["off2"][:4]), "little")
         if slot == 0xFFFFFFFF:
             assert rec[i]["nflags"] & 0x20
         else:
-            holders += 1
+            ids, _ = _chain(orec, oext, i)
+            spans.append((slot, slot + nsd.ext_words(len(ids))))
+            assert spans[-1][1] <= words
             assert _chain(rec, ext, i) == _chain(orec, oext, i)
-    assert holders == 1
+    assert (len(spans) >= 1) == (words >= 68)
+    spans.sort()
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
+    assert int(cnt[nsd.CNT_OVERFLOW]) >= len(need) - len(spans)
 
 
 @pytest.mark.parametrize("depth", [1, 3])
@@ -128,11 +134,12 @@ def test_pipe_batches(depth):
     batches = [T.make_batch(cfg, n, lo=lo) for cfg, n, lo in specs]
     max_pkts = max(len(d) for _, d in batches)
     max_bytes = max(f.nbytes for f, _ in batches)
-    pipe = nsd.Pipe(max_pkts, max_bytes, ext_cap=max_pkts, depth=depth)
+    words = nsd.ext_pool_words(max_pkts)
+    pipe = nsd.Pipe(max_pkts, max_bytes, ext_words=words, depth=depth)
     outs = []
     for frames, desc in batches:
         rec = np.zeros(len(desc), dtype=nsd.REC_DTYPE)
-        ext = np.zeros(max_pkts, dtype=nsd.EXT_DTYPE)
+        ext = np.zeros(words, dtype=np.uint32)
         ec = np.zeros(1, np.uint32)
         cnt = np.zeros(nsd.NCOUNTERS, np.uint64)
         st = np.full(1, -99, np.int32)

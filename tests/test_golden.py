@@ -40,8 +40,17 @@ def batch(name):
     return lt, pkts, frames, desc
 
 
+ICMPV6 = 11   # NSD_OPS_ICMPV6
+
+
 def host_only(texts_unsupported):
+    """Packets whose text the oracle does not restate (host-rendered leaves)."""
     return {i for i, (_, u) in enumerate(texts_unsupported) if u}
+
+
+def last_layer(r):
+    n = int(r["nflags"]) & 7
+    return (int(r["chain"]) >> (5 * (n - 1))) & 31 if 0 < n < 7 else -1
 
 
 @pytest.mark.parametrize("name", ["tiny", "edge"])
@@ -66,15 +75,22 @@ def test_formatter_matches_golden(name, mode):
     rec, ext, _, _ = T.oracle_records(frames, desc, linktype=lt, mode=mode)
     texts, rc = nsd.format_batch(frames, desc, rec, ext, mode=mode, linktype=lt)
     ora = T.oracle_text_packets(frames, desc, linktype=lt, mode=mode)
-    skip = host_only(ora) | {i for i in range(len(rec)) if rec[i]["nflags"] & 0x20}
+    hosted = host_only(ora)
+    rendered_leaves = 0
     for i in range(len(pkts)):
-        if i in skip:
+        if rec[i]["nflags"] & 0x20:          # overflow: the record holds no full chain
             assert rc[i] != 0
             continue
-        assert rc[i] == 0, f"packet {i}: formatter status {rc[i]}"
+        if rc[i] != 0:
+            # only bodies no host renderer covers yet (ICMPv6 130-154)
+            assert i in hosted and last_layer(rec[i]) == ICMPV6, f"packet {i}: status {rc[i]}"
+            continue
         assert texts[i] == gold[i], f"packet {i} differs"
+        rendered_leaves += i in hosted
     if name == "tiny":
-        assert not skip
+        assert not hosted
+    elif mode in (T.PRINT_NORM, T.PRINT_LESS):
+        assert rendered_leaves >= 4          # ARP, LLDP, IGMP, DCCP: text from the host leaves
 
 
 @pytest.mark.parametrize("name", ["tiny", "edge"])
@@ -111,10 +127,14 @@ def test_names_on(name, mode):
         nsd.lookup_cleanup()
         T.oracle().nsor_lookup_init(None)
     for i in range(len(pkts)):
-        if ora[i][1] or rec[i]["nflags"] & 0x20:
+        if rec[i]["nflags"] & 0x20:
             continue
-        assert ora[i][0] == gold[i], f"oracle packet {i}"
-        assert rc[i] == 0 and texts[i] == gold[i], f"formatter packet {i}"
+        if not ora[i][1]:
+            assert ora[i][0] == gold[i], f"oracle packet {i}"
+        if rc[i] != 0:
+            assert ora[i][1] and last_layer(rec[i]) == ICMPV6, f"formatter packet {i}: {rc[i]}"
+            continue
+        assert texts[i] == gold[i], f"formatter packet {i}"
 
 
 def test_prefix_digests():
