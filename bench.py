@@ -72,6 +72,45 @@ def cpu_baseline(cfg, n_sample, threads, seconds):
     return done / dt / 1e6, done, dt
 
 
+def bpf_bench(frames, desc, n, line_bytes, steps, warmup):
+    """Device BPF filter (nsd_bpf.hip) over the same resident batch:
+    bpfc.8's "Only allow IPv4 TCP packets" program (ldh [12]; jne #0x800;
+    ldb [23]; jneq #6; ret #-1; ret #0), verdicts only and with the compaction
+    of accepted descriptors.  Algorithmic bytes per packet: 8 (descriptor) +
+    the frame's first 64-B line (capped at caplen; the program reads bytes
+    12..23) + 4 (verdict); compaction adds 12 B read + 8 B per accepted packet.
+    Kernel time by HIP events on torch's current stream (the launch stream)."""
+    prog = np.array([(0x28, 0, 0, 12), (0x15, 0, 3, 0x800), (0x30, 0, 0, 23), (0x15, 0, 1, 6),
+                     (0x06, 0, 0, 0xFFFFFFFF), (0x06, 0, 0, 0)], dtype=nsd.BPF_INSN)
+    bp = nsd.BpfProgram(prog)
+    dev = desc.device
+    verdict = torch.empty(n, dtype=torch.int32, device=dev)
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = torch.empty(nsd.lib().nsd_bpf_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    res = {}
+    for compact in (False, True):
+        for _ in range(max(warmup, 1)):
+            bp.filter_device(frames, desc, compact, verdict, out, count, ws)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(steps):
+            bp.filter_device(frames, desc, compact, verdict, out, count, ws)
+        ev[1].record()
+        torch.cuda.synchronize()
+        res[compact] = ev[0].elapsed_time(ev[1]) / steps
+    kept = int(count.item())
+    algo = 8 * n + line_bytes + 4 * n
+    gbs = algo / (res[False] * 1e-3) / 1e9
+    bp.close()
+    return {"program": "bpfc.8 'Only allow IPv4 TCP packets' (6 insns)", "accepted": kept,
+            "value": round(n / (res[False] * 1e-3) / 1e6, 1), "unit": "Mpkt/s",
+            "kernel_ms": round(res[False], 4), "compact_ms": round(res[True], 4),
+            "compact_mpps": round(n / (res[True] * 1e-3) / 1e6, 1),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_pkt": round(algo / n, 2)}}
+
+
 def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
     """Host memory in, records in host memory out: `nbatch`
     batches of `batch` packets from one pinned host buffer go through the
@@ -139,6 +178,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="packets in the CPU sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline duration")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end pass")
+    ap.add_argument("--no-bpf", action="store_true", help="skip the device BPF filter pass")
     ap.add_argument("--e2e-batch", type=int, default=1 << 20)
     ap.add_argument("--e2e-batches", type=int, default=16)
     ap.add_argument("--e2e-depth", type=int, default=3)
@@ -163,6 +203,7 @@ def main():
     frames = torch.from_numpy(frames_np).to(dev)
     desc = torch.from_numpy(desc_np.view(np.int64)).to(dev)
     frame_bytes = int(T.desc_caplen(desc_np).sum())
+    line_bytes = int(np.minimum(T.desc_caplen(desc_np), 64).sum())   # first 64-B line per frame
     del frames_np
     ext_w = nsd.ext_pool_words(n) if args.config == "ipv6x" else nsd.ext_pool_words(n // 64)
     rec = torch.empty(n * REC_B, dtype=torch.uint8, device=dev)
@@ -220,6 +261,8 @@ def main():
     copy_gbs = 2 * cbuf.numel() * 5 / (ce[0].elapsed_time(ce[1]) * 1e-3) / 1e9
     del cbuf, cdst
 
+    bpf = None if args.no_bpf else bpf_bench(frames, desc, n, line_bytes, args.steps, args.warmup)
+
     cnt = counters.cpu().numpy().view(np.uint64)
     total_pkts = n * world
     assert int(cnt[nsd.CNT_PKTS]) == total_pkts, "counter check failed"
@@ -275,6 +318,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "bpf_filter": bpf,
         }
         print(json.dumps(out))
     if dist is not None:

@@ -8,9 +8,9 @@ profile files:
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE come
 from separate --pmc passes, in KiB; FETCH_SIZE counts half the bytes of a
 wide (16 B/lane) coalesced read on gfx950, so it is doubled; WRITE_SIZE is
-exact for 16 B/lane stores.  A dissect call is one dissect_fast launch plus
-the dissect_general / dissect_icmp launches that follow it; the per-call
-figure sums those kernels and divides by the number of calls."""
+exact for 16 B/lane stores.  A dissect call is one dissect_all launch (pass 1,
+pass 2 and the ICMPv4 checksums as phases of one kernel); the BPF filter
+kernels are reported separately (bpf_filter)."""
 import csv
 import json
 import os
@@ -21,16 +21,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PACKETS = 1 << 24
 
 
-def counter_sum(path, counter):
+def counter_sum(path, counter, kernel="nsd::dissect_all"):
     total, calls = 0.0, 0
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row["Kernel_Name"]
-            if "nsd::dissect" not in name or row["Counter_Name"] != counter:
+            if kernel not in name or row["Counter_Name"] != counter:
                 continue
             total += float(row["Counter_Value"])
-            if "dissect_fast" in name:
-                calls += 1
+            calls += 1
     return total, calls
 
 
@@ -58,8 +57,14 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "round")):
                    "WRITE_SIZE_KiB_per_call": wk / wc, "read_bytes_corrected": read_b,
                    "write_bytes": write_b, "hbm_bytes_per_launch": read_b + write_b,
                    "bytes_per_packet": (read_b + write_b) / PACKETS,
-                   "note": "per dissect call (fast + general + icmp kernels); read = 2 x FETCH_SIZE "
+                   "note": "per dissect_all launch; read = 2 x FETCH_SIZE "
                            "(gfx950 wide-read correction), KiB -> bytes"}
+            bk, bc = counter_sum(fp, "FETCH_SIZE", "bpf_filter<false>")
+            bw, bwc = counter_sum(wp, "WRITE_SIZE", "bpf_filter<false>")
+            if bc and bwc:
+                res["bpf_filter"] = {"read_bytes_corrected": 2 * bk * 1024 / bc, "write_bytes": bw * 1024 / bwc,
+                                     "hbm_bytes_per_launch": 2 * bk * 1024 / bc + bw * 1024 / bwc,
+                                     "launches": [bc, bwc]}
             with open(os.path.join(prof, f"pmc_{cfg}.json"), "w") as f:
                 json.dump(res, f, indent=1)
             print(cfg, json.dumps(res))
