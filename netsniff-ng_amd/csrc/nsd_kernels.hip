@@ -45,6 +45,9 @@ constexpr int row_of(int W) { return W / 4 + 1; }
 #ifndef NSD_MINW
 #define NSD_MINW 4                 // waves per SIMD the fused kernel is register-allocated for
 #endif
+#ifndef NSD_P1_TILES
+#define NSD_P1_TILES 16            // pass-1 grid strides per pass-2 round (0: whole shard)
+#endif
 #ifndef NSD_CSUM_SPLIT
 #define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
 #endif
@@ -415,7 +418,7 @@ template <int MODE>
 __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ frames,
 				      const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 				      uint4 *__restrict__ rec, uint4 *__restrict__ queue, uint32_t region,
-				      uint64_t *__restrict__ pend)
+				      uint64_t *__restrict__ pend, uint32_t first, uint32_t end, uint32_t &npend)
 {
 	constexpr int ROW = row_of(WIN1);
 	auto &s_win = sh.win;
@@ -429,13 +432,12 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 	uint4 *const bq = queue + (size_t)blockIdx.x * region;   // this block's queue region
 	// this wave's pending-checksum list (a wave visits region / WAVES packets)
 	uint64_t *const wq = pend + ((size_t)blockIdx.x * WAVES + wv) * (region / WAVES);
-	uint32_t npend = 0;
 	FlagCnt fc;
-	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
+	uint32_t base = first + blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
 
 	if (MODE != PRINT_NORM && MODE != PRINT_LESS) {
 		// every process() is NULL: no chain (dissector.c:51-53)
-		for (; base < n; base += stride) {
+		for (; base < end; base += stride) {
 			const uint32_t i = base + lane;
 			fc.pkts += FlagCnt::pc(i < n);
 			if (i < n) {
@@ -450,12 +452,14 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 
 	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
 	// descriptors are in flight
+	if (base >= end)
+		return;
 	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
-	uint64_t d1 = (base + stride + lane < n) ? desc[base + stride + lane] : 0;
+	uint64_t d1 = (base + stride < end && base + stride + lane < n) ? desc[base + stride + lane] : 0;
 	Chunks<WIN1> ch;
 	stage_load<false, WIN1>(ch, frames, d0, 0, lane);
 
-	for (; base < n; base += stride) {
+	for (; base < end; base += stride) {
 		const uint32_t i = base + lane;
 		const bool valid = i < n;
 		const uint64_t off = NSD_DESC_OFF(d0);
@@ -464,9 +468,9 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 		stage_write(&s_win[wv][0], ch, lane);
 		// prefetch: descriptors of tile t+2, chunks of tile t+1
 		const uint32_t b2 = base + 2 * stride;
-		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
+		const uint64_t d2 = (b2 < end && b2 + lane < n) ? desc[b2 + lane] : 0;
 		const uint32_t b1 = base + stride;
-		if (b1 < n)
+		if (b1 < end)
 			stage_load<false, WIN1>(ch, frames, d1, 0, lane);
 		wave_sync_lds();
 
@@ -540,8 +544,6 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 		d0 = d1;
 		d1 = d2;
 	}
-	if (lane == 0)
-		sh.pcnt[wv] = npend;
 	fc.flush(s_cnt, lane);
 }
 
@@ -554,11 +556,11 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 // window, emit the ended ones.  ICMPv4 messages past the window go to the
 // block's pass-2 pending list (sh.pn entries), ext chains to the ext pool.
 template <int MODE>
-__device__ __forceinline__ void pass2(Shared &sh, const uint8_t *__restrict__ frames,
+__device__ __forceinline__ uint32_t pass2(Shared &sh, const uint8_t *__restrict__ frames,
 				      const uint64_t *__restrict__ desc, int start_id, uint4 *__restrict__ rec,
 				      const uint4 *__restrict__ queue, uint32_t region,
 				      uint64_t *__restrict__ pend2, uint32_t *__restrict__ ext, uint32_t ext_words,
-				      uint32_t *__restrict__ ext_used, uint32_t chunk)
+				      uint32_t *__restrict__ ext_used, uint32_t chunk, uint32_t q0)
 {
 	constexpr int ROW = row_of(WIN2);
 	const int lane = threadIdx.x & 63;
@@ -578,7 +580,7 @@ __device__ __forceinline__ void pass2(Shared &sh, const uint8_t *__restrict__ fr
 	uint4 pe = make_uint4(0, 0, 0, 0);   // prefetched queue entry
 	uint64_t pd = 0;                      // its descriptor
 	bool pa = false, pb = false;          // entry in flight / entry + descriptor in flight
-	bool drained = nq == 0;               // wave-uniform: no queue entries left to take
+	bool drained = nq <= q0;              // wave-uniform: no queue entries left to take
 
 	for (;;) {
 		// (1) a lane without a packet takes its prefetched one
@@ -713,6 +715,7 @@ __device__ __forceinline__ void pass2(Shared &sh, const uint8_t *__restrict__ fr
 			wb = (w.data + m) & ~15u;
 	}
 	fc.flush(sh.cnt, lane);
+	return nq;
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
@@ -819,14 +822,28 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 		sh.wc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
 	block_init(sh.cnt, sh.lay3);   // (its barrier orders the stores above too)
 
-	pass1<MODE>(sh, frames, desc, n, start_id, rec, queue, region, pend);
-	if (MODE == PRINT_NORM || MODE == PRINT_LESS) {
-		__syncthreads();   // the block's queue and sh.qn are complete
+	// Pass 1 and pass 2 alternate over spans of NSD_P1_TILES grid strides, so
+	// a deferred packet is restaged while the lines pass 1 read are still in
+	// L2 / MALL (a whole-shard pass 1 first evicts them).
+	const uint32_t stride = gridDim.x * BLOCK;
+	const uint64_t span = NSD_P1_TILES ? (uint64_t)NSD_P1_TILES * stride : (uint64_t)n;
+	uint32_t npend = 0, q0 = 0;
+	for (uint64_t c0 = 0; c0 < n; c0 += span) {
+		const uint32_t end = (uint32_t)(c0 + span < n ? c0 + span : n);
+		pass1<MODE>(sh, frames, desc, n, start_id, rec, queue, region, pend, (uint32_t)c0, end, npend);
+		if (MODE == PRINT_NORM || MODE == PRINT_LESS) {
+			__syncthreads();   // the span's queue entries and sh.qn are complete
 #ifndef NSD_X_NOP2
-		pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, ext, ext_words, ext_used,
-			    chunk);
+			q0 = pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, ext, ext_words,
+					 ext_used, chunk, q0);
 #endif
+			__syncthreads();   // every wave is done taking entries: restart the taker at q0
+			if (threadIdx.x == 0)
+				sh.q2 = q0;
+		}
 	}
+	if ((threadIdx.x & 63) == 0)
+		sh.pcnt[threadIdx.x >> 6] = npend;
 	if (MODE == PRINT_NORM) {
 		__syncthreads();   // records final, pending lists and counts complete
 #ifndef NSD_X_NOICMP
