@@ -833,6 +833,8 @@ static void icmpv6_names(uint8_t t, uint8_t c, const char *&ts, const char *&cs,
 	}
 }
 
+static Done r_icmpv6_host(Out &o, const Frame &f, const Layer &L);
+
 // proto_icmpv6.c:1667-1699
 static Done r_icmpv6(Out &o, const Frame &f, const Layer &L, int mode)
 {
@@ -850,7 +852,7 @@ static Done r_icmpv6(Out &o, const Frame &f, const Layer &L, int mode)
 	int body;
 	icmpv6_names(type, code, ts, cs, body);
 	if (body < 0)
-		return { h, L.tail, false, false };   // host-only body (NSD_F_HOST)
+		return r_icmpv6_host(o, f, L);   // types 130-154 (NSD_F_HOST), nsd_format_icmpv6.h
 	uint32_t d = h + 4;
 	o << " [ ICMPv6 " << ts << " (";
 	o.u(type) << "), " << cs << " (";
@@ -920,6 +922,7 @@ static void dump_hex(Out &o, const Frame &f, uint32_t from, uint32_t len)
 }
 
 #include "nsd_format_leaves.h"
+#include "nsd_format_icmpv6.h"
 
 static bool is_lt(int lt, uint32_t v) { return (uint32_t)lt == v || (uint32_t)lt == __builtin_bswap32(v); }
 
@@ -1006,7 +1009,7 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 			dn = { L.start, L.tail, false, false };   // SLL, 802.11, netlink heads
 		}
 		if (!dn.ok)
-			return NSD_ERR_FORMAT;   // a body no host renderer covers yet (ICMPv6 130-154)
+			return NSD_ERR_FORMAT;
 		// consistency with the record: next layer's start / final cursor
 		if (k + 1 < n) {
 			if (!dn.next || dn.data != offs[k + 1])

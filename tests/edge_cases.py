@@ -174,9 +174,81 @@ def cases():
     add(eth(0x0800) + ipv4(2, 8) + bytes(8))                                 # IGMP
     add(eth(0x0800) + ipv4(33, 16) + bytes(16))                              # DCCP
     add(eth(0x86DD) + ipv6(58, 24) + bytes([135, 0]) + bytes(22))            # ICMPv6 NDP
+    icmpv6_bodies(add)
     return P
 
 
-# cases whose TEXT is outside this round's host renderer (ARP, LLDP, IGMP,
+def icmpv6_bodies(add):
+    """ICMPv6 types 130-154 (proto_icmpv6.c:1023-1474) and the Neighbor
+    Discovery options (:372-911): host-rendered bodies, every branch."""
+    A1 = bytes.fromhex("fe800000000000000211223344556677")
+    A2 = bytes.fromhex("ff020000000000000000000000000001")
+    A3 = bytes.fromhex("20010db8000000000000000000000042")
+
+    def i6(t, c, body):
+        add(eth(0x86DD) + ipv6(58, 4 + len(body)) + bytes([t, c]) + be16(0xBEEF) + body)
+
+    def opt(t, l8, payload):
+        return bytes([t, l8]) + payload
+
+    # MLD (130-132): v1, v2 (exponential delay, source list; nr_src is a
+    # uint8_t in print_ipv6_addr_list), short body
+    i6(130, 0, be16(1000) + be16(0) + A2)
+    i6(130, 0, be16(0x9123) + be16(7) + A2 + bytes([0x2A, 125]) + be16(2) + A1 + A3)
+    i6(130, 0, be16(10) + be16(0) + A2 + bytes([0x08, 1]) + be16(3) + A1)          # sources missing
+    i6(130, 0, be16(10) + be16(0) + A2 + bytes([0x00, 1]) + be16(0x0102) + A1 + A3 + b"xyz")
+    i6(130, 0, be16(10) + bytes(10))                                               # body pull fails
+    i6(131, 0, be16(0) + be16(0x55) + A2)
+    i6(132, 1, be16(3) + be16(0) + A2 + b"tail")
+    # Router / Neighbor Discovery with options
+    i6(133, 0, be32(0) + opt(1, 1, bytes.fromhex("001b21000001")) + opt(200, 1, bytes(6)))
+    i6(134, 0, bytes([64, 0xC0]) + be16(1800) + be32(30000) + be32(1000) +
+       opt(3, 4, bytes([64, 0xC0]) + be32(86400) + be32(14400) + be32(0) + A3) +
+       opt(5, 1, be16(0) + be32(1500)) + opt(25, 2, bytes(14)) + opt(31, 1, bytes(6)))
+    i6(135, 0, be32(0) + A1 + opt(1, 1, bytes.fromhex("3cfdfe000002")) + opt(2, 0, b""))   # len 0: invalid
+    i6(136, 0, be32(0xE0000005) + A1 + opt(2, 1, bytes.fromhex("3cfdfe000002")))
+    i6(137, 0, be32(0x01020304) + A1 + A3 + opt(4, 2, be16(0) + be32(0) + bytes(range(8))))
+    i6(134, 0, bytes([64, 0x40]) + be16(0) + be32(0) + be32(0) + opt(3, 2, bytes(14)) + bytes(20))  # opt 3 short
+    i6(133, 0, be32(0) + opt(1, 1, bytes(6)) + b"\x01")                          # option header pull fails
+    i6(133, 0, be32(0) + opt(9, 4, bytes(6)))                                    # option past the end
+    # Router Renumbering, Node Information
+    i6(138, 1, be32(77) + bytes([3, 0xA9]) + be16(500) + be32(0) + b"body")
+    i6(138, 7, be32(78) + bytes([0, 0x17]) + be16(0) + be32(9))
+    i6(139, 0, be16(2) + be16(0x1234) + bytes(range(1, 9)) + b"data")
+    i6(140, 2, be16(9) + be16(0) + bytes(8))
+    i6(139, 5, be16(4) + be16(1) + bytes(8))
+    # Inverse ND with address lists
+    i6(141, 0, be32(0) + opt(9, 5, be16(1) + be32(2) + A1 + A3))
+    i6(142, 0, be32(0) + opt(10, 3, be16(0) + be32(0) + A2) + opt(1, 1, bytes(6)))
+    # MLDv2 report: records, unknown record type, aux data, invalid aux length
+    i6(143, 0, be16(0) + be16(2) +
+       bytes([1, 1]) + be16(1) + A2 + A1 + b"\xaa\x0b\xcc\x0d" +
+       bytes([9, 0]) + be16(0) + A2)
+    i6(143, 0, be16(5) + be16(1) + bytes([0, 0]) + be16(0) + A2)
+    i6(143, 0, be16(0) + be16(1) + bytes([4, 9]) + be16(0) + A2 + bytes(8))
+    i6(143, 0, be16(0) + be16(2) + bytes([6, 0]) + be16(0) + A2)                 # second record missing
+    # Mobile IPv6 (144-147)
+    i6(144, 0, be16(42) + be16(0))
+    i6(145, 0, be16(42) + be16(1) + A1 + A3 + b"12345")
+    i6(146, 0, be16(43) + be16(2))
+    # option 15 (name type, size_t pad length): valid, pad past the option
+    i6(147, 0, be16(44) + be16(0xC005) +
+       opt(15, 2, bytes([2]) + (2).to_bytes(8, "little") + b"a\x07b" + b"\x01\x02"))
+    i6(147, 0, be16(44) + be16(0x4000) + opt(15, 2, bytes([7]) + (99).to_bytes(8, "little") + bytes(5)))
+    # SEND (148-149): options 16, 17 (20-byte form and the wrong-length branch)
+    i6(148, 0, be16(1) + be16(2) + opt(16, 1, bytes([1, 0x33]) + b"\xde\xad\xbe\xef"))
+    i6(149, 0, be16(1) + be16(3) + be16(2) + be16(0) +
+       opt(17, 3, bytes([2, 64]) + b"\x01\x00\x00\x00" + A3) + opt(17, 2, bytes([9, 48]) + bytes(range(12))))
+    # 150-154 and option 19
+    i6(150, 0, bytes([0x11, 0x22, 0x33, 0x44]) + b"opts")
+    i6(151, 0, be16(20) + be16(2))
+    i6(152, 0, b"")
+    i6(153, 0, b"\x09")
+    i6(154, 0, bytes([1, 2]) + be16(300) + opt(19, 1, bytes([4]) + bytes.fromhex("0011223344")) +
+       opt(19, 1, bytes([9]) + bytes(5)))
+    i6(154, 3, bytes([1, 2]))                                                    # body pull fails
+
+
+# cases whose text is rendered by host leaves (ARP, LLDP, IGMP,
 # DCCP, ICMPv6 130-154) or outside the parity domain; records still compared
 HOST_ONLY_TEXT = {"arp", "lldp", "igmp", "dccp", "icmpv6-ndp"}

@@ -13,6 +13,7 @@
                        C2/C3/C4 (NORM, LESS) and of the oracle records / counters
   wsum.json            sum of W(pkt) (algorithmic read bytes) over
                        the 16M-packet shards used by bench.py
+  (--edge-only: the two pcaps and their texts only)
 
 IPv4/IPv6 layers inside nsref come from the restatement (their reference
 sources need the configure-generated config.h); see oracle/ref_harness.c.
@@ -77,6 +78,8 @@ def main():
         for m in (T.PRINT_NORM, T.PRINT_LESS):
             save_text(f"{stem}.m{m}.w80", T.run_ref(pcap, mode=m, cols=0))
             save_text(f"{stem}.names.m{m}.w65535", T.run_ref(pcap, mode=m, cols=65535, names=True))
+    if "--edge-only" in sys.argv:
+        return
 
     prefix = {}
     for key, cfg in (("udp64", T.SYN_UDP64), ("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):

@@ -76,21 +76,21 @@ def test_formatter_matches_golden(name, mode):
     texts, rc = nsd.format_batch(frames, desc, rec, ext, mode=mode, linktype=lt)
     ora = T.oracle_text_packets(frames, desc, linktype=lt, mode=mode)
     hosted = host_only(ora)
-    rendered_leaves = 0
+    rendered_leaves = icmpv6_bodies = 0
     for i in range(len(pkts)):
         if rec[i]["nflags"] & 0x20:          # overflow: the record holds no full chain
             assert rc[i] != 0
             continue
-        if rc[i] != 0:
-            # only bodies no host renderer covers yet (ICMPv6 130-154)
-            assert i in hosted and last_layer(rec[i]) == ICMPV6, f"packet {i}: status {rc[i]}"
-            continue
+        assert rc[i] == 0, f"packet {i}: status {rc[i]}"
         assert texts[i] == gold[i], f"packet {i} differs"
         rendered_leaves += i in hosted
+        icmpv6_bodies += i in hosted and last_layer(rec[i]) == ICMPV6
     if name == "tiny":
         assert not hosted
     elif mode in (T.PRINT_NORM, T.PRINT_LESS):
         assert rendered_leaves >= 4          # ARP, LLDP, IGMP, DCCP: text from the host leaves
+    if name == "edge" and mode == T.PRINT_NORM:
+        assert icmpv6_bodies >= 40           # ICMPv6 130-154 bodies (nsd_format_icmpv6.h)
 
 
 @pytest.mark.parametrize("name", ["tiny", "edge"])
@@ -131,9 +131,7 @@ def test_names_on(name, mode):
             continue
         if not ora[i][1]:
             assert ora[i][0] == gold[i], f"oracle packet {i}"
-        if rc[i] != 0:
-            assert ora[i][1] and last_layer(rec[i]) == ICMPV6, f"formatter packet {i}: {rc[i]}"
-            continue
+        assert rc[i] == 0, f"formatter packet {i}: {rc[i]}"
         assert texts[i] == gold[i], f"formatter packet {i}"
 
 
