@@ -265,7 +265,9 @@ def main():
 
     cnt = counters.cpu().numpy().view(np.uint64)
     total_pkts = n * world
-    assert int(cnt[nsd.CNT_PKTS]) == total_pkts, "counter check failed"
+    # (experiment builds that skip a phase on purpose set NSD_BENCH_NOCHECK)
+    assert int(cnt[nsd.CNT_PKTS]) == total_pkts or os.environ.get("NSD_BENCH_NOCHECK"), \
+        "counter check failed"
     ms_per_step = elapsed / args.steps * 1e3
     mpps = total_pkts * args.steps / elapsed / 1e6
 

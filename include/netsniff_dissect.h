@@ -276,6 +276,32 @@ int nsd_pipe_wait(nsd_pipe *p);
 int nsd_pipe_drain(nsd_pipe *p);
 void nsd_pipe_destroy(nsd_pipe *p);
 
+/* ---- pcap replay front end (`netsniff-ng --in f.pcap`, read_pcap
+ * netsniff-ng.c:640-770; pcap_io.h / pcap_sg.c record formats) ---------------
+ * nsd_pcap_open: validates the file header (tcpdump usec / nsec, Kuznetzov,
+ * Borkmann magics, either byte order, version 2.4; SLL / netlink files use the
+ * *_LL record form), NULL on error.  nsd_pcap_linktype: the header's link
+ * type as stored (byte-swapped files pass it swapped, as the reference does).
+ * nsd_pcap_read_batch: reads up to max_n records into frames[0, cap) at
+ * 16-byte aligned offsets (NSD_FRAME_PAD zero bytes kept after the last),
+ * desc[k] = NSD_DESC(offset, caplen); wire_len / ts_ns (may be NULL) receive
+ * the record lengths and timestamps.  Returns the records read, 0 at the end
+ * (a record with caplen 0 or above 1 MiB ends the replay like pcap_sg_read's
+ * -EINVAL), or NSD_ERR_ARG.
+ * nsd_replay_pcap: the whole replay loop: read -> optional device BPF filter
+ * -> pipelined device walk -> formatter -> [tprintf wrap at `cols` > 0] ->
+ * out_fd, in file order; counters (may be NULL) accumulates the counter
+ * vector.  Returns the records printed or a negative NSD_ERR_*. */
+typedef struct nsd_pcap nsd_pcap;
+struct nsd_bpf_prog;
+nsd_pcap *nsd_pcap_open(const char *path);
+int nsd_pcap_linktype(const nsd_pcap *p);
+long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
+			 uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns);
+void nsd_pcap_close(nsd_pcap *p);
+long nsd_replay_pcap(const char *path, int mode, const struct nsd_bpf_prog *filter, int out_fd,
+		     int cols, uint64_t *counters);
+
 /* ---- classic BPF on the device --------------------------------
  * The capture loop filters every record before dissecting it (read_pcap
  * netsniff-ng.c:707-725: bpf_run_filter, bpf.c:508-705, skips the record on

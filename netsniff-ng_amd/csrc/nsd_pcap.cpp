@@ -1,0 +1,358 @@
+// nsd_pcap.cpp - the pcap replay front end of the dissector path
+// (`netsniff-ng --in file.pcap`, read_pcap netsniff-ng.c:640-770): a pcap
+// reader that packs records into batches (frames + nsd_desc_t), and a replay
+// driver that feeds them through the optional device BPF filter and the
+// pipelined device walk (nsd_pipe_*) and writes the formatted text.
+//
+// Reader semantics follow pcap_io.h and pcap_sg.c:
+//   - file header validation and the *_LL remap for SLL / netlink files
+//     (pcap_validate_header, pcap_io.h:874-908); the link type handed to the
+//     dissector is the header field as stored, so a byte-swapped file passes
+//     a byte-swapped link type (pcap_generic_pull_fhdr :910-928), which the
+//     entry point matches either way (dissector.c:79);
+//   - record header sizes per format (pcap_get_hdr_length :429-452: 16 for
+//     usec / nsec, 32 for the *_LL forms whose 16-byte cooked header is not
+//     packet data, 24 for the Kuznetzov / Borkmann forms), the caplen field
+//     byte-swapped for swapped files and minus 16 for *_LL
+//     (pcap_get_length :322-352);
+//   - a record with caplen 0 or above the 1 MiB replay buffer ends the
+//     replay, as pcap_sg_read's -EINVAL does (pcap_sg.c:121-123), and so
+//     does a short read at the end of the file.
+#include <errno.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/netsniff_dissect.h"
+
+extern "C" long nsd_format_batch(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
+				 int linktype, int mode, const nsd_rec *rec, const uint32_t *ext_pool,
+				 char *out, size_t cap, uint64_t *ends, int8_t *rc);
+
+namespace {
+
+constexpr uint32_t TCPDUMP = 0xa1b2c3d4, NSEC = 0xa1b23c4d, KUZ = 0xa1b2cd34, BKM = 0xa1e2cb12;
+constexpr uint32_t LT_LINUX_SLL = 113, LT_NETLINK = 253;
+constexpr uint32_t REPLAY_BUF = 1024 * 1024;   // read_pcap's `out` buffer (netsniff-ng.c:680)
+
+uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+uint16_t bswap16(uint16_t v) { return __builtin_bswap16(v); }
+
+} // namespace
+
+struct nsd_pcap {
+	int fd = -1;
+	bool swapped = false;
+	uint32_t hdrsize = 16;   // record header bytes (pcap_get_hdr_length)
+	uint32_t ll_extra = 0;   // cooked-header bytes counted in caplen (*_LL)
+	uint32_t linktype = 0;   // as stored in the file header
+	bool nsec = false;
+	bool eof = false;
+	// buffered reader (the scatter-gather reader's iovecs, pcap_sg.c)
+	std::vector<uint8_t> buf;
+	size_t pos = 0, len = 0;
+
+	bool fill(size_t need)
+	{
+		if (len - pos >= need)
+			return true;
+		if (pos) {
+			memmove(buf.data(), buf.data() + pos, len - pos);
+			len -= pos;
+			pos = 0;
+		}
+		if (buf.size() < need)
+			buf.resize(need);
+		while (len < need) {
+			ssize_t r = read(fd, buf.data() + len, buf.size() - len);
+			if (r < 0 && errno == EINTR)
+				continue;
+			if (r <= 0)
+				return false;
+			len += (size_t)r;
+		}
+		return true;
+	}
+};
+
+extern "C" nsd_pcap *nsd_pcap_open(const char *path)
+{
+	if (!path)
+		return nullptr;
+	int fd = open(path, O_RDONLY);
+	if (fd < 0)
+		return nullptr;
+	nsd_pcap *p = new nsd_pcap;
+	p->fd = fd;
+	p->buf.resize(4 << 20);
+	uint8_t h[24];
+	if (!p->fill(24)) {
+		nsd_pcap_close(p);
+		return nullptr;
+	}
+	memcpy(h, p->buf.data(), 24);
+	p->pos = 24;
+	uint32_t magic, lt;
+	memcpy(&magic, h, 4);
+	memcpy(&lt, h + 20, 4);
+	uint16_t vmaj, vmin;
+	memcpy(&vmaj, h + 4, 2);
+	memcpy(&vmin, h + 6, 2);
+	// pcap_check_magic (pcap_io.h:286-320)
+	uint32_t m = magic;
+	if (m == bswap32(TCPDUMP) || m == bswap32(NSEC) || m == bswap32(KUZ) || m == bswap32(BKM)) {
+		p->swapped = true;
+		m = bswap32(m);
+	}
+	if (m != TCPDUMP && m != NSEC && m != KUZ && m != BKM) {
+		nsd_pcap_close(p);
+		return nullptr;
+	}
+	// pcap_validate_header: version 2.4 in either byte order
+	if ((vmaj != 2 && bswap16(vmaj) != 2) || (vmin != 4 && bswap16(vmin) != 4)) {
+		nsd_pcap_close(p);
+		return nullptr;
+	}
+	const uint32_t lt_host = p->swapped ? bswap32(lt) : lt;
+	p->linktype = lt;
+	p->nsec = m == NSEC || m == BKM;
+	if (m == KUZ || m == BKM) {
+		p->hdrsize = 24;
+	} else if (lt_host == LT_LINUX_SLL || lt_host == LT_NETLINK) {
+		p->hdrsize = 32;   // *_LL: the cooked header follows the record header
+		p->ll_extra = 16;
+	}
+	return p;
+}
+
+extern "C" int nsd_pcap_linktype(const nsd_pcap *p) { return p ? (int)p->linktype : -1; }
+
+extern "C" void nsd_pcap_close(nsd_pcap *p)
+{
+	if (!p)
+		return;
+	if (p->fd >= 0)
+		close(p->fd);
+	delete p;
+}
+
+// Read up to max_n records into frames[0, cap): frames packed at 16-byte
+// aligned offsets (TPACKET_ALIGNMENT, as in the RX ring), NSD_FRAME_PAD bytes
+// kept free past the last one.  desc[k] = NSD_DESC(offset, caplen);
+// wire_len[k] (may be NULL) = the record's original length, ts_ns[k] (may be
+// NULL) = its timestamp in ns.  Returns the records read (0 at the end of the
+// replay), or NSD_ERR_ARG.
+extern "C" long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
+				    uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns)
+{
+	if (!p || !frames || !desc || cap < NSD_FRAME_PAD)
+		return NSD_ERR_ARG;
+	size_t off = 0;
+	uint32_t n = 0;
+	while (n < max_n && !p->eof) {
+		if (!p->fill(p->hdrsize)) {
+			p->eof = true;
+			break;
+		}
+		const uint8_t *h = p->buf.data() + p->pos;
+		uint32_t sec, frac, cl, wl;
+		memcpy(&sec, h, 4);
+		memcpy(&frac, h + 4, 4);
+		memcpy(&cl, h + 8, 4);
+		memcpy(&wl, h + 12, 4);
+		if (p->swapped) {
+			sec = bswap32(sec);
+			frac = bswap32(frac);
+			cl = bswap32(cl);
+			wl = bswap32(wl);
+		}
+		const uint32_t caplen = cl - p->ll_extra;   // unsigned, as the reference computes it
+		if (caplen == 0 || caplen > REPLAY_BUF || caplen > NSD_MAX_CAPLEN) {
+			p->eof = true;   // pcap_sg_read: -EINVAL ends read_pcap's loop
+			break;
+		}
+		const size_t at = (off + 15) & ~(size_t)15;
+		if (at + caplen + NSD_FRAME_PAD > cap) {
+			if (n == 0)
+				return NSD_ERR_ARG;   // one record does not fit the batch buffer
+			break;                        // next batch
+		}
+		if (!p->fill((size_t)p->hdrsize + caplen)) {
+			p->eof = true;
+			break;
+		}
+		h = p->buf.data() + p->pos;
+		memcpy(frames + at, h + p->hdrsize, caplen);
+		p->pos += p->hdrsize + caplen;
+		desc[n] = NSD_DESC(at, caplen);
+		if (wire_len)
+			wire_len[n] = wl;
+		if (ts_ns)
+			ts_ns[n] = (uint64_t)sec * 1000000000ull + (p->nsec ? frac : (uint64_t)frac * 1000ull);
+		off = at + caplen;
+		n++;
+	}
+	memset(frames + off, 0, NSD_FRAME_PAD);
+	return n;
+}
+
+// The replay loop: read -> [BPF filter on the device] -> device walk (pipelined,
+// `depth` batches in flight) -> host formatter -> [tprintf wrap] -> out_fd.
+// Writes the text dissector_entry_point prints for each accepted record, in
+// file order.  `filter` may be NULL (every record passes, bpf.c:711).
+// `cols` > 0 wraps like tprintf at that width, 0 writes the unwrapped stream.
+// counters (may be NULL) accumulates the per-protocol counter vector.
+// Returns the records printed, or a negative NSD_ERR_*.
+extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *filter, int out_fd,
+				int cols, uint64_t *counters)
+{
+	constexpr uint32_t BATCH = 1u << 16;
+	constexpr size_t FRAME_BYTES = 64ull << 20;
+	constexpr int DEPTH = 3;
+	nsd_pcap *p = nsd_pcap_open(path);
+	if (!p)
+		return NSD_ERR_ARG;
+	const int lt = (int)p->linktype;
+	const uint32_t ext_words = 64 * BATCH;
+	nsd_pipe *pipe = nsd_pipe_create(BATCH, FRAME_BYTES, ext_words, DEPTH, lt, mode);
+	if (!pipe) {
+		nsd_pcap_close(p);
+		return NSD_ERR_HIP;
+	}
+	struct Batch {
+		uint8_t *frames = nullptr;
+		nsd_desc_t *desc = nullptr;
+		nsd_rec *rec = nullptr;
+		uint32_t *ext = nullptr;
+		uint32_t *verdict = nullptr;
+		uint32_t ext_used = 0, n = 0;
+		uint64_t cnt[NSD_NCOUNTERS];
+		int status = 0;
+		bool busy = false;
+	};
+	Batch b[DEPTH];
+	long rc = 0, printed = 0;
+	long wrap_state = 0;
+	std::string text, wrapped;
+	for (auto &x : b) {
+		x.frames = (uint8_t *)nsd_host_alloc(FRAME_BYTES);
+		x.desc = (nsd_desc_t *)nsd_host_alloc(BATCH * sizeof(nsd_desc_t));
+		x.rec = (nsd_rec *)nsd_host_alloc(BATCH * sizeof(nsd_rec));
+		x.ext = (uint32_t *)nsd_host_alloc(ext_words * sizeof(uint32_t));
+		x.verdict = (uint32_t *)malloc(BATCH * sizeof(uint32_t));
+		if (!x.frames || !x.desc || !x.rec || !x.ext || !x.verdict)
+			rc = NSD_ERR_NOMEM;
+	}
+	// complete the oldest batch and print it
+	auto finish = [&](Batch &x) -> long {
+		int st = nsd_pipe_wait(pipe);
+		x.busy = false;
+		if (st != NSD_OK)
+			return st < 0 ? st : NSD_ERR_HIP;
+		if (x.status != NSD_OK)
+			return x.status;
+		if (counters)
+			for (int k = 0; k < NSD_NCOUNTERS; k++)
+				counters[k] += x.cnt[k];
+		size_t cap = 1 << 20;
+		for (;;) {
+			text.resize(cap);
+			long t = nsd_format_batch(x.frames, x.desc, x.n, lt, mode, x.rec, x.ext, &text[0], cap,
+						  nullptr, nullptr);
+			if (t >= 0) {
+				text.resize((size_t)t);
+				break;
+			}
+			cap = (size_t)(-t);
+		}
+		const char *w = text.data();
+		size_t wn = text.size();
+		if (cols > 0 && wn) {
+			wrapped.resize(2 * wn + 16);
+			long k = nsd_tprintf_wrap(text.data(), wn, cols, &wrap_state, &wrapped[0], wrapped.size());
+			if (k < 0)
+				return k;
+			w = wrapped.data();
+			wn = (size_t)k;
+		}
+		while (wn) {
+			ssize_t r = write(out_fd, w, wn);
+			if (r < 0 && errno == EINTR)
+				continue;
+			if (r <= 0)
+				return NSD_ERR_ARG;
+			w += r;
+			wn -= (size_t)r;
+		}
+		printed += x.n;
+		return NSD_OK;
+	};
+	int slot = 0;
+	while (rc == NSD_OK) {
+		Batch &x = b[slot];
+		if (x.busy && (rc = finish(x)) != NSD_OK)
+			break;
+		long n = nsd_pcap_read_batch(p, x.frames, FRAME_BYTES, x.desc, BATCH, nullptr, nullptr);
+		if (n < 0) {
+			rc = n;
+			break;
+		}
+		if (n == 0)
+			break;
+		size_t used = 0;
+		for (long k = 0; k < n; k++) {
+			const size_t e = NSD_DESC_OFF(x.desc[k]) + NSD_DESC_CAPLEN(x.desc[k]);
+			used = e > used ? e : used;
+		}
+		if (filter) {
+			// bpf_run_filter per record before the dissector (netsniff-ng.c:723-725)
+			int r = nsd_bpf_filter_batch(filter, x.frames, used, x.desc, (uint32_t)n, x.verdict);
+			if (r != NSD_OK) {
+				rc = r;
+				break;
+			}
+			long m = 0;
+			for (long k = 0; k < n; k++)
+				if (x.verdict[k])
+					x.desc[m++] = x.desc[k];
+			n = m;
+			if (n == 0)
+				continue;
+		}
+		x.n = (uint32_t)n;
+		memset(x.cnt, 0, sizeof(x.cnt));
+		int r = nsd_pipe_submit(pipe, x.frames, used, x.desc, x.n, x.rec, x.ext, &x.ext_used, x.cnt,
+					&x.status);
+		if (r != NSD_OK) {
+			rc = r;
+			break;
+		}
+		x.busy = true;
+		slot = (slot + 1) % DEPTH;
+	}
+	// drain in submission order
+	for (int k = 0; k < DEPTH; k++) {
+		Batch &x = b[(slot + k) % DEPTH];
+		if (x.busy) {
+			long r = finish(x);
+			if (rc == NSD_OK)
+				rc = r;
+		}
+	}
+	for (auto &x : b) {
+		nsd_host_free(x.frames);
+		nsd_host_free(x.desc);
+		nsd_host_free(x.rec);
+		nsd_host_free(x.ext);
+		free(x.verdict);
+	}
+	nsd_pipe_destroy(pipe);
+	nsd_pcap_close(p);
+	return rc == NSD_OK ? printed : rc;
+}

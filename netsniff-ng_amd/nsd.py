@@ -66,7 +66,9 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_pipe_create", "nsd_pipe_submit", "nsd_pipe_wait", "nsd_pipe_drain",
                "nsd_pipe_destroy", "nsd_host_alloc", "nsd_host_free", "nsd_host_register",
                "nsd_host_unregister", "nsd_bpf_validate", "nsd_bpf_load", "nsd_bpf_free",
-               "nsd_bpf_workspace_bytes", "nsd_bpf_filter_device", "nsd_bpf_filter_batch"]
+               "nsd_bpf_workspace_bytes", "nsd_bpf_filter_device", "nsd_bpf_filter_batch",
+               "nsd_pcap_open", "nsd_pcap_linktype", "nsd_pcap_read_batch", "nsd_pcap_close",
+               "nsd_replay_pcap"]
 
 _lib = None
 _vp, _u32, _u64, _int, _sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
@@ -142,6 +144,16 @@ def lib():
         L.nsd_bpf_filter_device.argtypes = [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
         L.nsd_bpf_filter_batch.restype = _int
         L.nsd_bpf_filter_batch.argtypes = [_vp, _vp, _sz, _vp, _u32, _vp]
+        L.nsd_pcap_open.restype = _vp
+        L.nsd_pcap_open.argtypes = [ctypes.c_char_p]
+        L.nsd_pcap_linktype.restype = _int
+        L.nsd_pcap_linktype.argtypes = [_vp]
+        L.nsd_pcap_read_batch.restype = ctypes.c_long
+        L.nsd_pcap_read_batch.argtypes = [_vp, _vp, _sz, _vp, _u32, _vp, _vp]
+        L.nsd_pcap_close.restype = None
+        L.nsd_pcap_close.argtypes = [_vp]
+        L.nsd_replay_pcap.restype = ctypes.c_long
+        L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp]
         _lib = L
     return _lib
 
@@ -379,3 +391,45 @@ class BpfProgram:
 
     def __del__(self):
         self.close()
+
+
+# ---- pcap replay front end (nsd_pcap.cpp) ---------------------------------------
+def pcap_read(path, cap=64 << 20, max_n=1 << 16):
+    """Read a whole pcap through nsd_pcap_read_batch: (linktype, [batches]),
+    each batch = (frames uint8, desc uint64, wire_len uint32, ts_ns uint64)."""
+    L = lib()
+    h = L.nsd_pcap_open(os.fsencode(path))
+    if not h:
+        raise NsdError(f"nsd_pcap_open({path}) failed")
+    try:
+        lt = L.nsd_pcap_linktype(h)
+        out = []
+        while True:
+            frames = np.zeros(cap, dtype=np.uint8)
+            desc = np.zeros(max_n, dtype=np.uint64)
+            wl = np.zeros(max_n, dtype=np.uint32)
+            ts = np.zeros(max_n, dtype=np.uint64)
+            n = L.nsd_pcap_read_batch(h, frames.ctypes.data, cap, desc.ctypes.data, max_n,
+                                      wl.ctypes.data, ts.ctypes.data)
+            if n < 0:
+                raise NsdError(f"nsd_pcap_read_batch failed with status {n}")
+            if n == 0:
+                return lt, out
+            out.append((frames, desc[:n], wl[:n], ts[:n]))
+    finally:
+        L.nsd_pcap_close(h)
+
+
+def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None):
+    """`netsniff-ng --in path` through the device: returns (records printed,
+    text bytes).  prog: a BpfProgram (or None)."""
+    import tempfile
+    L = lib()
+    cnt = counters if counters is not None else np.zeros(NCOUNTERS, dtype=np.uint64)
+    with tempfile.TemporaryFile() as f:
+        n = L.nsd_replay_pcap(os.fsencode(path), mode, prog.h if prog is not None else None,
+                              f.fileno(), cols, cnt.ctypes.data)
+        if n < 0:
+            raise NsdError(f"nsd_replay_pcap failed with status {n}")
+        f.seek(0)
+        return n, f.read()

@@ -1,0 +1,166 @@
+"""pcap replay front end (nsd_pcap.cpp; read_pcap netsniff-ng.c:640-770,
+pcap_io.h record formats, pcap_sg.c reader).
+
+CPU: the reader against the committed pcaps (tiny = C1, edge) in every record
+format the reference reads (usec / nsec / Kuznetzov / Borkmann magics, both
+byte orders, the *_LL form of SLL files), batch splitting and the end-of-replay
+rules.  GPU: the whole `--in` loop (reader -> [device BPF] -> pipelined
+device walk -> formatter -> [tprintf wrap]) reproduces the golden text the
+reference's parser objects printed for the same files."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import nsd
+import nsd_testlib as T
+import test_golden as TG
+
+G = T.GOLDEN
+
+
+def packets_of(path, **kw):
+    lt, batches = nsd.pcap_read(path, **kw)
+    out = []
+    for frames, desc, wl, ts in batches:
+        for d in desc:
+            d = int(d)
+            off, cl = d & 0xFFFFFFFFFF, d >> 40
+            assert off % 16 == 0
+            out.append(bytes(frames[off:off + cl]))
+    return lt, out, batches
+
+
+def rewrite(pkts, path, magic=0xA1B2C3D4, endian="<", linktype=1, rec_extra=b"", ll=False):
+    """Write pkts in a given pcap record format (pcap_io.h:43-116)."""
+    with open(path, "wb") as f:
+        f.write(struct.pack(endian + "IHHiIII", magic, 2, 4, 0, 0, 65535, linktype))
+        for i, p in enumerate(pkts):
+            cooked = bytes(range(16)) if ll else b""
+            f.write(struct.pack(endian + "IIII", 1000 + i, 7 * i, len(p) + len(cooked), len(p) + 3))
+            f.write(rec_extra + cooked + bytes(p))
+
+
+@pytest.mark.parametrize("name", ["tiny", "edge"])
+def test_reader_matches_pcap(name):
+    lt, want = T.read_pcap(os.path.join(G, name + ".pcap"))
+    got_lt, got, batches = packets_of(os.path.join(G, name + ".pcap"))
+    # the replay ends at the first zero-length record (pcap_sg_read /
+    # pcap_mm_read return -EINVAL, read_pcap leaves its loop)
+    if b"" in want:
+        want = want[:want.index(b"")]
+        assert name == "edge" and want
+    assert got_lt == lt and got == want
+    # the frames after the last one are zero (NSD_FRAME_PAD)
+    frames, desc = batches[-1][0], batches[-1][1]
+    end = int(desc[-1]) & 0xFFFFFFFFFF
+    end += int(desc[-1]) >> 40
+    assert not frames[end:end + 64].any()
+
+
+@pytest.mark.parametrize("fmt", ["usec_be", "nsec", "nsec_be", "kuz", "bkm", "bkm_be", "sll", "sll_be"])
+def test_reader_record_formats(tmp_path, fmt):
+    pkts = [p for p in T.read_pcap(os.path.join(G, "edge.pcap"))[1] if p][:40]
+    path = str(tmp_path / "f.pcap")
+    spec = {
+        "usec_be": dict(endian=">"),
+        "nsec": dict(magic=0xA1B23C4D),
+        "nsec_be": dict(magic=0xA1B23C4D, endian=">"),
+        "kuz": dict(magic=0xA1B2CD34, rec_extra=bytes(8)),
+        "bkm": dict(magic=0xA1E2CB12, rec_extra=bytes(8)),
+        "bkm_be": dict(magic=0xA1E2CB12, endian=">", rec_extra=bytes(8)),
+        "sll": dict(linktype=113, ll=True),
+        "sll_be": dict(linktype=113, ll=True, endian=">"),
+    }[fmt]
+    rewrite(pkts, path, **spec)
+    lt, got, batches = packets_of(path)
+    want_lt = spec.get("linktype", 1)
+    if spec.get("endian") == ">":
+        want_lt = int.from_bytes(want_lt.to_bytes(4, "big"), "little")   # passed as stored
+    assert lt == want_lt
+    assert got == pkts
+    wl = np.concatenate([b[2] for b in batches])
+    ts = np.concatenate([b[3] for b in batches])
+    assert list(wl) == [len(p) + 3 for p in pkts]
+    nsec = fmt.startswith("nsec") or fmt.startswith("bkm")
+    assert list(ts) == [(1000 + i) * 10**9 + 7 * i * (1 if nsec else 1000) for i in range(len(pkts))]
+
+
+def test_reader_batches_and_end_rules(tmp_path):
+    pkts = [p for p in T.read_pcap(os.path.join(G, "edge.pcap"))[1] if p]
+    full = str(tmp_path / "full.pcap")
+    T.write_pcap(full, pkts)
+    # small buffers split the file into several batches, in order
+    lt, got, batches = packets_of(full, cap=4096, max_n=7)
+    assert got == pkts and len(batches) > 1 and all(len(b[1]) <= 7 for b in batches)
+    # a zero-length record ends the replay (pcap_sg_read -EINVAL), as does a
+    # truncated last record
+    path = str(tmp_path / "z.pcap")
+    rewrite(pkts[:5] + [b""] + pkts[5:9], path)
+    assert packets_of(path)[1] == pkts[:5]
+    data = open(full, "rb").read()
+    path2 = str(tmp_path / "t.pcap")
+    open(path2, "wb").write(data[:-3])
+    assert packets_of(path2)[1] == pkts[:-1]
+    # bad magic / version
+    bad = str(tmp_path / "b.pcap")
+    open(bad, "wb").write(b"\x00" * 24)
+    with pytest.raises(nsd.NsdError):
+        nsd.pcap_read(bad)
+
+
+MODES = [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX, T.PRINT_ASCII, T.PRINT_HEX_ASCII]
+
+
+def replayable(name, mode, tmp_path):
+    """The committed pcap minus the records the replay cannot print as the
+    golden does: zero-length ones (they end the reference's replay) and
+    layer-budget overflows (no full chain in the record).  Returns (path,
+    kept indices)."""
+    lt, pkts = T.read_pcap(os.path.join(G, name + ".pcap"))
+    rec, _, _, _ = T.oracle_records(*T.batch_from_packets(pkts), linktype=lt, mode=mode)
+    keep = [i for i in range(len(pkts)) if pkts[i] and not rec[i]["nflags"] & 0x20]
+    path = str(tmp_path / (name + ".pcap"))
+    T.write_pcap(path, [pkts[i] for i in keep], linktype=lt)
+    return path, keep
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["tiny", "edge"])
+@pytest.mark.parametrize("mode", MODES)
+def test_replay_matches_golden(tmp_path, name, mode):
+    """`--in file.pcap` end to end on the device == the reference's text."""
+    gold = TG.load_golden(f"{name}.m{mode}.w65535")
+    path, keep = replayable(name, mode, tmp_path)
+    if name == "tiny":
+        assert len(keep) == 1000
+    cnt = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
+    n, text = nsd.replay_pcap(path, mode=mode, counters=cnt)
+    assert n == len(keep)
+    assert text == b"".join(gold[i] for i in keep)
+    assert int(cnt[nsd.CNT_PKTS]) == len(keep)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_replay_wrapped_and_filtered(tmp_path, mode):
+    """80-column tprintf wrap over the replay stream, and a BPF filter in
+    front (only the accepted records print, in file order)."""
+    _, pkts = T.read_pcap(os.path.join(G, "edge.pcap"))
+    path, keep = replayable("edge", mode, tmp_path)
+    unwrapped = TG.load_golden(f"edge.m{mode}.w65535")
+    n, text = nsd.replay_pcap(path, mode=mode, cols=80)
+    state, want = 0, b""
+    for i in keep:
+        w, state = nsd.tprintf_wrap(unwrapped[i], cols=80, state=state)
+        want += w
+    assert n == len(keep) and text == want
+    # bpfc.8 "IPv4 TCP" program: ldh [12]; jeq #0x800 ...; ldb [23]; jeq #6; ret #-1; ret #0
+    prog = np.array([(0x28, 0, 0, 12), (0x15, 0, 3, 0x800), (0x30, 0, 0, 23), (0x15, 0, 1, 6),
+                     (0x06, 0, 0, 0xFFFFFFFF), (0x06, 0, 0, 0)], dtype=nsd.BPF_INSN)
+    bp = nsd.BpfProgram(prog)
+    acc = [i for i in keep if len(pkts[i]) >= 24 and pkts[i][12:14] == b"\x08\x00" and pkts[i][23] == 6]
+    assert acc
+    n, text = nsd.replay_pcap(path, mode=mode, prog=bp)
+    assert n == len(acc) and text == b"".join(unwrapped[i] for i in acc)

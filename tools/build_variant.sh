@@ -10,7 +10,7 @@ mkdir -p $d
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function $*"
 $H -c netsniff-ng_amd/csrc/nsd_kernels.hip -o $d/k.o
 objs="$d/k.o"
-for f in nsd_bpf nsd_host nsd_pipe nsd_format nsd_lookup; do
+for f in nsd_bpf nsd_host nsd_pipe nsd_format nsd_lookup nsd_pcap; do
   [ netsniff-ng_amd/build/$f.o -nt netsniff-ng_amd/csrc/$f.cpp ] || [ netsniff-ng_amd/build/$f.o -nt netsniff-ng_amd/csrc/$f.hip ] || make -s -C netsniff-ng_amd
   objs="$objs netsniff-ng_amd/build/$f.o"
 done
