@@ -165,6 +165,33 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
                     "(nsd_pipe_*), best of %d passes" % reps}
 
 
+def replay_leg(cfg, n, mode, threads, reps=2):
+    """`netsniff-ng --in file.pcap` through the device (nsd_replay_pcap): a
+    synthetic pcap of n records in a temp file -> reader -> pipelined device
+    walk -> host formatter on `threads` threads -> /dev/null.  Reported
+    beside the device-resident number; never `value`."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "replay.pcap")
+        T.synth().nsd_synth_pcap(cfg, T.SEED, 0, n, path.encode())
+        size = os.path.getsize(path)
+        fd = os.open(os.devnull, os.O_WRONLY)
+        try:
+            best = None
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                got, _ = nsd.replay_pcap(path, mode=mode, threads=threads, out_fd=fd)
+                dt = time.perf_counter() - t0
+                assert got == n
+                best = dt if best is None else min(best, dt)
+        finally:
+            os.close(fd)
+    return {"value": round(n / best / 1e6, 3), "unit": "Mpkt/s", "packets": n,
+            "file_gbs": round(size / best / 1e9, 2), "format_threads": threads,
+            "note": "pcap file -> nsd_pcap reader -> H2D -> dissect kernels -> D2H -> host text "
+                    "formatter -> /dev/null (nsd_replay_pcap), best of %d" % reps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -179,6 +206,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline duration")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end pass")
     ap.add_argument("--no-bpf", action="store_true", help="skip the device BPF filter pass")
+    ap.add_argument("--no-replay", action="store_true", help="skip the pcap replay (--in) pass")
+    ap.add_argument("--replay-packets", type=int, default=1 << 20)
     ap.add_argument("--e2e-batch", type=int, default=1 << 20)
     ap.add_argument("--e2e-batches", type=int, default=16)
     ap.add_argument("--e2e-depth", type=int, default=3)
@@ -305,6 +334,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = end_to_end(c["cfg"], args.e2e_batch, args.e2e_batches, args.e2e_depth, args.mode)
 
+    replay = None
+    if rank == 0 and world == 1 and not args.no_replay:
+        replay = replay_leg(c["cfg"], args.replay_packets, args.mode, min(os.cpu_count() or 1, 16))
+
     if rank == 0:
         out = {
             "metric": "Mpkt/s + GB/s device-resident dissect, 64B & IMIX; bit-exact fields vs ref",
@@ -320,6 +353,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "replay": replay,
             "bpf_filter": bpf,
         }
         print(json.dumps(out))

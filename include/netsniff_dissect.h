@@ -291,7 +291,8 @@ void nsd_pipe_destroy(nsd_pipe *p);
  * nsd_replay_pcap: the whole replay loop: read -> optional device BPF filter
  * -> pipelined device walk -> formatter -> [tprintf wrap at `cols` > 0] ->
  * out_fd, in file order; counters (may be NULL) accumulates the counter
- * vector.  Returns the records printed or a negative NSD_ERR_*. */
+ * vector; `threads` host threads format each batch (<= 0: up to 16).
+ * Returns the records printed or a negative NSD_ERR_*. */
 typedef struct nsd_pcap nsd_pcap;
 struct nsd_bpf_prog;
 nsd_pcap *nsd_pcap_open(const char *path);
@@ -300,7 +301,7 @@ long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *d
 			 uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns);
 void nsd_pcap_close(nsd_pcap *p);
 long nsd_replay_pcap(const char *path, int mode, const struct nsd_bpf_prog *filter, int out_fd,
-		     int cols, uint64_t *counters);
+		     int cols, uint64_t *counters, int threads);
 
 /* ---- classic BPF on the device --------------------------------
  * The capture loop filters every record before dissecting it (read_pcap

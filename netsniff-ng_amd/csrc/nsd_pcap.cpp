@@ -27,6 +27,7 @@
 #include <unistd.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/netsniff_dissect.h"
@@ -208,10 +209,17 @@ extern "C" long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, ns
 // file order.  `filter` may be NULL (every record passes, bpf.c:711).
 // `cols` > 0 wraps like tprintf at that width, 0 writes the unwrapped stream.
 // counters (may be NULL) accumulates the per-protocol counter vector.
+// `threads` host threads render each batch (<= 0: up to 16 by the hardware).
 // Returns the records printed, or a negative NSD_ERR_*.
 extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *filter, int out_fd,
-				int cols, uint64_t *counters)
+				int cols, uint64_t *counters, int threads)
 {
+	if (threads <= 0) {
+		const unsigned hc = std::thread::hardware_concurrency();
+		threads = hc ? (int)(hc < 16 ? hc : 16) : 1;
+	}
+	if (threads > 64)
+		threads = 64;
 	constexpr uint32_t BATCH = 1u << 16;
 	constexpr size_t FRAME_BYTES = 64ull << 20;
 	constexpr int DEPTH = 3;
@@ -260,17 +268,39 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 		if (counters)
 			for (int k = 0; k < NSD_NCOUNTERS; k++)
 				counters[k] += x.cnt[k];
-		size_t cap = 1 << 20;
-		for (;;) {
-			text.resize(cap);
-			long t = nsd_format_batch(x.frames, x.desc, x.n, lt, mode, x.rec, x.ext, &text[0], cap,
-						  nullptr, nullptr);
-			if (t >= 0) {
-				text.resize((size_t)t);
-				break;
+		// render the batch on `threads` host threads over contiguous packet
+		// ranges (records are independent; only the wrap carries state), then
+		// join the pieces in order
+		const uint32_t nt = x.n < 2048 ? 1u : (uint32_t)threads;
+		std::vector<std::string> part(nt);
+		std::vector<long> prc(nt, 0);
+		auto render = [&](uint32_t t) {
+			const uint32_t lo = (uint32_t)((uint64_t)x.n * t / nt), hi = (uint32_t)((uint64_t)x.n * (t + 1) / nt);
+			size_t cap = 256 * (size_t)(hi - lo) + 4096;
+			for (;;) {
+				part[t].resize(cap);
+				long r = nsd_format_batch(x.frames, x.desc + lo, hi - lo, lt, mode, x.rec + lo, x.ext,
+							  &part[t][0], cap, nullptr, nullptr);
+				if (r >= 0) {
+					part[t].resize((size_t)r);
+					break;
+				}
+				cap = (size_t)(-r);
 			}
-			cap = (size_t)(-t);
+		};
+		if (nt == 1) {
+			render(0);
+		} else {
+			std::vector<std::thread> th;
+			for (uint32_t t = 1; t < nt; t++)
+				th.emplace_back(render, t);
+			render(0);
+			for (auto &h : th)
+				h.join();
 		}
+		text.clear();
+		for (auto &q : part)
+			text += q;
 		const char *w = text.data();
 		size_t wn = text.size();
 		if (cols > 0 && wn) {

@@ -153,7 +153,7 @@ def lib():
         L.nsd_pcap_close.restype = None
         L.nsd_pcap_close.argtypes = [_vp]
         L.nsd_replay_pcap.restype = ctypes.c_long
-        L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp]
+        L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp, _int]
         _lib = L
     return _lib
 
@@ -420,15 +420,20 @@ def pcap_read(path, cap=64 << 20, max_n=1 << 16):
         L.nsd_pcap_close(h)
 
 
-def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None):
+def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None, threads=0, out_fd=None):
     """`netsniff-ng --in path` through the device: returns (records printed,
-    text bytes).  prog: a BpfProgram (or None)."""
+    text bytes), or (records printed, None) when writing to out_fd.
+    prog: a BpfProgram (or None)."""
     import tempfile
     L = lib()
     cnt = counters if counters is not None else np.zeros(NCOUNTERS, dtype=np.uint64)
+    h = prog.h if prog is not None else None
+    if out_fd is not None:
+        n = L.nsd_replay_pcap(os.fsencode(path), mode, h, out_fd, cols, cnt.ctypes.data, threads)
+        _check(0 if n >= 0 else n, "nsd_replay_pcap")
+        return n, None
     with tempfile.TemporaryFile() as f:
-        n = L.nsd_replay_pcap(os.fsencode(path), mode, prog.h if prog is not None else None,
-                              f.fileno(), cols, cnt.ctypes.data)
+        n = L.nsd_replay_pcap(os.fsencode(path), mode, h, f.fileno(), cols, cnt.ctypes.data, threads)
         if n < 0:
             raise NsdError(f"nsd_replay_pcap failed with status {n}")
         f.seek(0)

@@ -136,7 +136,7 @@ def test_replay_matches_golden(tmp_path, name, mode):
     if name == "tiny":
         assert len(keep) == 1000
     cnt = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
-    n, text = nsd.replay_pcap(path, mode=mode, counters=cnt)
+    n, text = nsd.replay_pcap(path, mode=mode, counters=cnt, threads=1 if name == "edge" else 4)
     assert n == len(keep)
     assert text == b"".join(gold[i] for i in keep)
     assert int(cnt[nsd.CNT_PKTS]) == len(keep)
@@ -164,3 +164,21 @@ def test_replay_wrapped_and_filtered(tmp_path, mode):
     assert acc
     n, text = nsd.replay_pcap(path, mode=mode, prog=bp)
     assert n == len(acc) and text == b"".join(unwrapped[i] for i in acc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key,cfg", [("udp64", T.SYN_UDP64), ("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_replay_prefix_digest(tmp_path, key, cfg, mode):
+    """64K-packet synthetic pcaps (C2/C3/C4 prefixes) replayed through the
+    device with 8 formatting threads: the text's SHA-256 equals the digest of
+    the reference parser objects' text (tests/golden/prefix.json)."""
+    import hashlib
+    import json
+    with open(os.path.join(G, "prefix.json")) as f:
+        want = json.load(f)[f"{key}:m{mode}"]["text_sha256"]
+    path = str(tmp_path / f"{key}.pcap")
+    T.synth().nsd_synth_pcap(cfg, T.SEED, 0, 65536, path.encode())
+    n, text = nsd.replay_pcap(path, mode=mode, threads=8)
+    assert n == 65536
+    assert hashlib.sha256(text).hexdigest() == want

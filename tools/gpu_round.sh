@@ -21,7 +21,7 @@ for cfg in imix ipv6x; do
   echo "bench $cfg rc=$rc"; fatal $rc bench
 done
 cd /tmp && export TMPDIR=/tmp
-ARGS="--no-cpu --no-e2e --steps 10 --warmup 2"
+ARGS="--no-cpu --no-e2e --no-replay --steps 10 --warmup 2"
 for cfg in udp64 imix ipv6x; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/stats_$cfg" -o run --output-format csv -- python3 "$R/bench.py" --config $cfg $ARGS > "$O/stats_$cfg.log" 2>&1; rc=$?
   echo "stats $cfg rc=$rc"; fatal $rc stats

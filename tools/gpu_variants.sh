@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 for v in $VARS; do
   if [ "$v" = base ]; then unset NSD_LIB; else export NSD_LIB=$R/variants/$v/libnsdissect.so; fi
   for cfg in ${CFG:-udp64}; do
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/${v}_$cfg" -o run --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 5 --warmup 1 --no-cpu --no-e2e ${BENCH_ARGS} > "$O/${v}_$cfg.log" 2>&1; rc=$?
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/${v}_$cfg" -o run --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 5 --warmup 1 --no-cpu --no-e2e --no-replay ${BENCH_ARGS} > "$O/${v}_$cfg.log" 2>&1; rc=$?
     echo "== $v $cfg rc=$rc"; [ $rc = 0 ] || { tail -5 "$O/${v}_$cfg.log"; exit $rc; }
     f=$(find "$O/${v}_$cfg" -name '*kernel_stats.csv' | head -n 1)
     python3 - "$f" <<'PY'
