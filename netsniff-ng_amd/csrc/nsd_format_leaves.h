@@ -207,7 +207,7 @@ static void igmp_csum(Out &o, const Frame &f, uint32_t m, uint32_t len)
 	o << ", CSum (0x";
 	o.xn(f.be16(m + 2), 4) << ") is ";
 	if (cs) {
-		o << C_RED << "bogus (!)" << C_END << " - " << C_RED << "should be ";
+		o << C_RED << "bogus (!)" << C_END << " - " << C_RED << " should be ";   // " - %s should be %x%s"
 		o.x(csum_expected(f.le16(m + 2), cs)) << C_END;
 	} else {
 		o << "ok";
