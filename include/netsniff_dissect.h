@@ -303,6 +303,19 @@ void nsd_pcap_close(nsd_pcap *p);
 long nsd_replay_pcap(const char *path, int mode, const struct nsd_bpf_prog *filter, int out_fd,
 		     int cols, uint64_t *counters, int threads);
 
+/* ---- TPACKET_V3 RX ring front end (walk_t3_block, netsniff-ng.c:990-1039) --
+ * nsd_t3_block_desc: descriptors for the frames of one retired ring block
+ * (tpacket_block_desc + tpacket3_hdr chain), pointing into the block itself:
+ * submit the block as the batch's frame buffer (nsd_pipe_submit(block,
+ * block_len, desc, n, ...)) and hand it back to the kernel when that batch
+ * completes (the reference hands it back after the whole block,
+ * netsniff-ng.c:1121).  skip_packet (netsniff-ng.c:425-442): packet_type >= 0
+ * keeps only that sll_pkttype, else loopback (lo_ifindex) PACKET_OUTGOING
+ * frames are dropped.  Returns the frames described, or NSD_ERR_ARG for an
+ * inconsistent block or more than max_n frames. */
+long nsd_t3_block_desc(const uint8_t *block, size_t block_len, int packet_type, int lo_ifindex,
+		       nsd_desc_t *desc, uint32_t max_n);
+
 /* ---- classic BPF on the device --------------------------------
  * The capture loop filters every record before dissecting it (read_pcap
  * netsniff-ng.c:707-725: bpf_run_filter, bpf.c:508-705, skips the record on

@@ -386,3 +386,54 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 	nsd_pcap_close(p);
 	return rc == NSD_OK ? printed : rc;
 }
+
+// ---- TPACKET_V3 ring front end (walk_t3_block, netsniff-ng.c:990-1039) ------
+// A retired RX ring block (struct block_desc, netsniff-ng.c:1061-1066 =
+// tpacket_block_desc: version, offset_to_priv, tpacket_hdr_v1 {block_status,
+// num_pkts, offset_to_first_pkt, blk_len, seq_num, ts_first, ts_last}) is
+// turned into descriptors that point into the block itself, so the block
+// is the batch's frame buffer (zero copy on the host; nsd_pipe_submit(block,
+// block_len, desc, n, ...)).  Per frame: tpacket3_hdr {tp_next_offset,
+// tp_sec, tp_nsec, tp_snaplen, tp_len, tp_status, tp_mac, tp_net, ...} with the
+// sockaddr_ll at TPACKET_ALIGN(sizeof(tpacket3_hdr)) = 48 after it; the packet
+// is at hdr + tp_mac, tp_snaplen bytes.  skip_packet (netsniff-ng.c:425-442):
+// with packet_type >= 0 only frames of that sll_pkttype are kept; otherwise
+// frames on the loopback ifindex `lo_ifindex` with PACKET_OUTGOING (4) are
+// dropped.  Returns the frames described, or NSD_ERR_ARG for a block whose
+// headers point outside it (or a frame above NSD_MAX_CAPLEN).
+extern "C" long nsd_t3_block_desc(const uint8_t *block, size_t block_len, int packet_type,
+				  int lo_ifindex, nsd_desc_t *desc, uint32_t max_n)
+{
+	if (!block || !desc || block_len < 48)
+		return NSD_ERR_ARG;
+	uint32_t num_pkts, first;
+	memcpy(&num_pkts, block + 12, 4);
+	memcpy(&first, block + 16, 4);
+	size_t h = first;
+	uint32_t n = 0;
+	for (uint32_t i = 0; i < num_pkts; i++) {
+		if (h + 48 + 20 > block_len)
+			return NSD_ERR_ARG;
+		uint32_t next, snaplen;
+		uint16_t mac;
+		int32_t ifindex;
+		memcpy(&next, block + h, 4);
+		memcpy(&snaplen, block + h + 12, 4);
+		memcpy(&mac, block + h + 24, 2);
+		memcpy(&ifindex, block + h + 48 + 4, 4);
+		const uint8_t pkttype = block[h + 48 + 10];
+		const bool skip = packet_type >= 0 ? pkttype != (uint8_t)packet_type
+						   : (ifindex == lo_ifindex && pkttype == 4);
+		if (!skip) {
+			if (h + mac + (size_t)snaplen > block_len || snaplen > NSD_MAX_CAPLEN || n >= max_n)
+				return NSD_ERR_ARG;
+			desc[n++] = NSD_DESC(h + mac, snaplen);
+		}
+		if (i + 1 < num_pkts) {
+			if (next == 0)
+				return NSD_ERR_ARG;
+			h += next;
+		}
+	}
+	return n;
+}

@@ -68,7 +68,7 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_host_unregister", "nsd_bpf_validate", "nsd_bpf_load", "nsd_bpf_free",
                "nsd_bpf_workspace_bytes", "nsd_bpf_filter_device", "nsd_bpf_filter_batch",
                "nsd_pcap_open", "nsd_pcap_linktype", "nsd_pcap_read_batch", "nsd_pcap_close",
-               "nsd_replay_pcap"]
+               "nsd_replay_pcap", "nsd_t3_block_desc"]
 
 _lib = None
 _vp, _u32, _u64, _int, _sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
@@ -152,6 +152,8 @@ def lib():
         L.nsd_pcap_read_batch.argtypes = [_vp, _vp, _sz, _vp, _u32, _vp, _vp]
         L.nsd_pcap_close.restype = None
         L.nsd_pcap_close.argtypes = [_vp]
+        L.nsd_t3_block_desc.restype = ctypes.c_long
+        L.nsd_t3_block_desc.argtypes = [_vp, _sz, _int, _int, _vp, _u32]
         L.nsd_replay_pcap.restype = ctypes.c_long
         L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp, _int]
         _lib = L
@@ -438,3 +440,13 @@ def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None, threads
             raise NsdError(f"nsd_replay_pcap failed with status {n}")
         f.seek(0)
         return n, f.read()
+
+
+def t3_block_desc(block, packet_type=-1, lo_ifindex=-1, max_n=1 << 16):
+    """Descriptors of a TPACKET_V3 block's frames (nsd_t3_block_desc)."""
+    block = np.ascontiguousarray(block, dtype=np.uint8)
+    desc = np.zeros(max_n, dtype=np.uint64)
+    n = lib().nsd_t3_block_desc(block.ctypes.data, block.nbytes, packet_type, lo_ifindex,
+                                desc.ctypes.data, max_n)
+    _check(0 if n >= 0 else n, "nsd_t3_block_desc")
+    return desc[:n]

@@ -1,0 +1,86 @@
+"""TPACKET_V3 RX ring front end (nsd_t3_block_desc; walk_t3_block
+netsniff-ng.c:990-1039, struct block_desc :1061-1066, linux/if_packet.h
+tpacket3_hdr / tpacket_hdr_v1 layouts): synthetic retired blocks built here,
+frames at hdr + tp_mac, skip_packet rules; on the GPU the block itself is the
+batch's frame buffer and the records equal the oracle's."""
+import struct
+
+import numpy as np
+import pytest
+
+import edge_cases
+import nsd
+import nsd_testlib as T
+
+PACKET_HOST, PACKET_OUTGOING = 0, 4
+
+
+def make_block(pkts, pkttypes=None, ifindex=None, block_len=1 << 20, mac_pad=2):
+    """tpacket_block_desc (48 B) + per frame tpacket3_hdr (48 B) + sockaddr_ll
+    (20 B) + pad so the MAC header sits at 2 mod 16 (as the kernel places it),
+    frames TPACKET_ALIGN'ed (16)."""
+    blk = bytearray(block_len)
+    first = 48
+    h = first
+    offs = []
+    for i, p in enumerate(pkts):
+        mac = ((48 + 20 + 15) & ~15) + mac_pad      # TPACKET_ALIGN(hdr + sll) + NET_IP_ALIGN-ish
+        nxt = (mac + len(p) + 15) & ~15
+        last = i == len(pkts) - 1
+        hdr = struct.pack("<IIIIIIHH", 0 if last else nxt, 1000 + i, 7 * i, len(p), len(p) + 4, 1, mac, mac + 14)
+        blk[h:h + len(hdr)] = hdr
+        pt = pkttypes[i] if pkttypes else PACKET_HOST
+        ix = ifindex[i] if ifindex else 2
+        sll = struct.pack("<HHiHBB8s", 17, 0x0008, ix, 1, pt, 6, bytes(8))
+        blk[h + 48:h + 48 + 20] = sll
+        blk[h + mac:h + mac + len(p)] = p
+        offs.append(h + mac)
+        h += nxt
+    struct.pack_into("<IIIIIIQ", blk, 0, 3, 0, 1, len(pkts), first, h, 9)
+    return np.frombuffer(bytes(blk[:h + 64]), dtype=np.uint8).copy(), offs
+
+
+def test_block_desc_frames():
+    pkts = [p for p in edge_cases.cases() if p][:90]
+    blk, offs = make_block(pkts)
+    desc = nsd.t3_block_desc(blk)
+    assert [int(d) & 0xFFFFFFFFFF for d in desc] == offs
+    assert [bytes(blk[int(d) & 0xFFFFFFFFFF:][:int(d) >> 40]) for d in desc] == pkts
+    assert all(o % 16 == 2 for o in offs)
+
+
+def test_block_skip_packet_rules():
+    pkts = [p for p in edge_cases.cases() if p][:20]
+    types = [PACKET_OUTGOING if i % 3 == 0 else PACKET_HOST for i in range(20)]
+    ifx = [1 if i % 2 == 0 else 2 for i in range(20)]
+    blk, offs = make_block(pkts, types, ifx)
+    # default: loopback (ifindex 1) outgoing frames are skipped
+    d = nsd.t3_block_desc(blk, packet_type=-1, lo_ifindex=1)
+    assert [int(x) & 0xFFFFFFFFFF for x in d] == [o for i, o in enumerate(offs) if not (ifx[i] == 1 and types[i] == 4)]
+    # -t outgoing: only PACKET_OUTGOING frames
+    d = nsd.t3_block_desc(blk, packet_type=PACKET_OUTGOING, lo_ifindex=1)
+    assert [int(x) & 0xFFFFFFFFFF for x in d] == [o for i, o in enumerate(offs) if types[i] == 4]
+
+
+def test_block_inconsistent():
+    pkts = [p for p in edge_cases.cases() if p][:5]
+    blk, _ = make_block(pkts)
+    bad = blk.copy()
+    struct.pack_into("<I", bad, 12, 50)            # more frames than the chain holds
+    with pytest.raises(nsd.NsdError):
+        nsd.t3_block_desc(bad)
+    with pytest.raises(nsd.NsdError):
+        nsd.t3_block_desc(blk[:200])               # headers past the block
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_block_dissect_on_device(mode):
+    from test_device_parity import assert_same_records
+    pkts = [p for p in edge_cases.cases() if p]
+    blk, _ = make_block(pkts)
+    desc = nsd.t3_block_desc(blk)
+    rec, ext, cnt = nsd.entry_batch(blk, desc, mode=mode)
+    orec, oext, ocnt, _ = T.oracle_records(blk, desc, mode=mode)
+    assert_same_records(rec, orec, ext, oext)
+    assert np.array_equal(cnt, ocnt)
