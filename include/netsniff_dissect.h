@@ -276,6 +276,35 @@ int nsd_pipe_wait(nsd_pipe *p);
 int nsd_pipe_drain(nsd_pipe *p);
 void nsd_pipe_destroy(nsd_pipe *p);
 
+/* ---- LINKTYPE_LINUX_SLL heads (dissector_sll.c:39-82) -----------------------
+ * The SLL "cooked" head prints the packet's struct sockaddr_ll (pkt->sll,
+ * dissector.c:74: the RX ring's per-frame sockaddr_ll, or the *_LL pcap
+ * record's cooked header) and, in print_full, continues in eth_lay2 with
+ * sll_protocol when the hatype maps to Ethernet (pcap_devtype_to_linktype).
+ * nsd_sll_t is struct sockaddr_ll's layout (20 bytes).  Batches of an SLL
+ * link type pass one per packet (NULL reads as zeros). */
+typedef struct nsd_sll {
+	uint16_t family;
+	uint16_t protocol;   /* network byte order */
+	int32_t  ifindex;
+	uint16_t hatype;
+	uint8_t  pkttype;
+	uint8_t  halen;
+	uint8_t  addr[8];
+} nsd_sll_t;
+int nsd_dissect_device_sll(const uint8_t *d_frames, const nsd_desc_t *d_desc,
+			   const nsd_sll_t *d_sll, uint32_t n, int linktype, int mode,
+			   nsd_rec *d_rec, uint32_t *d_ext, uint32_t ext_words,
+			   uint32_t *d_ext_used, uint64_t *d_counters, void *d_workspace,
+			   void *stream);
+int dissector_entry_batch_sll(const uint8_t *frames, size_t frames_len,
+			      const nsd_desc_t *desc, const nsd_sll_t *sll, uint32_t n,
+			      int linktype, int mode, nsd_rec *rec, uint32_t *ext,
+			      uint32_t ext_words, uint32_t *ext_used, uint64_t *counters);
+long nsd_format_packet_sll(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+			   const nsd_rec *rec, const uint32_t *ext_pool, const nsd_sll_t *sll,
+			   char *out, size_t cap);
+
 /* ---- pcap replay front end (`netsniff-ng --in f.pcap`, read_pcap
  * netsniff-ng.c:640-770; pcap_io.h / pcap_sg.c record formats) ---------------
  * nsd_pcap_open: validates the file header (tcpdump usec / nsec, Kuznetzov,

@@ -923,12 +923,13 @@ static void dump_hex(Out &o, const Frame &f, uint32_t from, uint32_t len)
 
 #include "nsd_format_leaves.h"
 #include "nsd_format_icmpv6.h"
+#include "nsd_format_sll.h"
 
 static bool is_lt(int lt, uint32_t v) { return (uint32_t)lt == v || (uint32_t)lt == __builtin_bswap32(v); }
 
 // Render one packet; returns NSD_OK or NSD_ERR_FORMAT (text so far kept).
 int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-		  const nsd_rec &rec, const uint32_t *ext_pool)
+		  const nsd_rec &rec, const uint32_t *ext_pool, const nsd_sll_t *sll)
 {
 	Out o(s);
 	Frame f{ pkt, caplen };
@@ -1005,8 +1006,9 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 		case NSD_OPS_LLDP:           dn = r_lldp(o, f, L, mode); break;
 		case NSD_OPS_IGMP:           dn = r_igmp(o, f, L, mode); break;
 		case NSD_OPS_DCCP:           dn = r_dccp(o, f, L, mode); break;
+		case NSD_OPS_SLL:            dn = r_sll(o, L, mode, sll); break;
 		default:
-			dn = { L.start, L.tail, false, false };   // SLL, 802.11, netlink heads
+			dn = { L.start, L.tail, false, false };   // 802.11, netlink heads
 		}
 		if (!dn.ok)
 			return NSD_ERR_FORMAT;
@@ -1062,13 +1064,20 @@ void format_post_dump(std::string &s, const uint8_t *pkt, uint32_t caplen, int m
 extern "C" long nsd_format_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
 				  const nsd_rec *rec, const uint32_t *ext_pool, char *out, size_t cap)
 {
+	return nsd_format_packet_sll(pkt, caplen, linktype, mode, rec, ext_pool, nullptr, out, cap);
+}
+
+extern "C" long nsd_format_packet_sll(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+				      const nsd_rec *rec, const uint32_t *ext_pool, const nsd_sll_t *sll,
+				      char *out, size_t cap)
+{
 	if (!pkt && caplen)
 		return NSD_ERR_ARG;
 	if (!rec)
 		return NSD_ERR_ARG;
 	std::string s;
 	s.reserve(256 + 6 * (size_t)caplen);
-	int rc = nsd::format_packet(s, pkt, caplen, linktype, mode, *rec, ext_pool);
+	int rc = nsd::format_packet(s, pkt, caplen, linktype, mode, *rec, ext_pool, sll);
 	if (out && cap) {
 		size_t k = s.size() < cap - 1 ? s.size() : cap - 1;
 		memcpy(out, s.data(), k);
@@ -1082,16 +1091,30 @@ extern "C" long nsd_format_packet(const uint8_t *pkt, uint32_t caplen, int linkt
 // Batch formatter: renders packets [0, n) into one buffer; per-packet end
 // offsets in ends[] (so callers can split), status per packet in rc[] (may be
 // NULL).  Returns total bytes, or -needed when cap is too small.
+extern "C" long nsd_format_batch_sll(const uint8_t *frames, const nsd_desc_t *desc,
+				     const nsd_sll_t *sll, uint32_t n, int linktype, int mode,
+				     const nsd_rec *rec, const uint32_t *ext_pool, char *out, size_t cap,
+				     uint64_t *ends, int8_t *rc);
+
 extern "C" long nsd_format_batch(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
 				 int linktype, int mode, const nsd_rec *rec, const uint32_t *ext_pool,
 				 char *out, size_t cap, uint64_t *ends, int8_t *rc)
+{
+	return nsd_format_batch_sll(frames, desc, nullptr, n, linktype, mode, rec, ext_pool, out, cap, ends, rc);
+}
+
+// same, with one sockaddr_ll per packet (SLL link types; may be NULL)
+extern "C" long nsd_format_batch_sll(const uint8_t *frames, const nsd_desc_t *desc,
+				     const nsd_sll_t *sll, uint32_t n, int linktype, int mode,
+				     const nsd_rec *rec, const uint32_t *ext_pool, char *out, size_t cap,
+				     uint64_t *ends, int8_t *rc)
 {
 	std::string s;
 	s.reserve(cap ? cap : 4096);
 	for (uint32_t i = 0; i < n; i++) {
 		const uint64_t d = desc[i];
 		int r = nsd::format_packet(s, frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), linktype,
-					   mode, rec[i], ext_pool);
+					   mode, rec[i], ext_pool, sll ? sll + i : nullptr);
 		if (rc)
 			rc[i] = (int8_t)r;
 		if (ends)

@@ -19,6 +19,10 @@
 
 #include "../../include/netsniff_dissect.h"
 
+extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
+				      uint32_t n, int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
+				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
+				      void *d_ws, int grid, hipStream_t stream);
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
 				  int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
 				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
@@ -27,7 +31,7 @@ extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
 
 namespace nsd {
 int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-		  const nsd_rec &rec, const uint32_t *ext_pool);
+		  const nsd_rec &rec, const uint32_t *ext_pool, const nsd_sll_t *sll = nullptr);
 void format_post_dump(std::string &s, const uint8_t *pkt, uint32_t caplen, int mode, uint32_t from,
 		      uint32_t to);
 }
@@ -87,6 +91,7 @@ struct DevCtx {
 	uint64_t *counters = nullptr;
 	uint8_t *ws = nullptr; size_t ws_cap = 0;          // queue for entry_batch
 	uint8_t *dev_ws = nullptr; size_t dev_ws_cap = 0;  // nsd_dissect_device's own
+	uint8_t *sll = nullptr; size_t sll_cap = 0;        // per-packet sockaddr_ll (SLL heads)
 };
 DevCtx g_ctx;
 
@@ -221,10 +226,35 @@ extern "C" int nsd_dissect_device(const uint8_t *d_frames, const nsd_desc_t *d_d
 	return rc ? NSD_ERR_HIP : NSD_OK;
 }
 
+extern "C" int nsd_dissect_device_sll(const uint8_t *d_frames, const nsd_desc_t *d_desc,
+				      const nsd_sll_t *d_sll, uint32_t n, int linktype, int mode,
+				      nsd_rec *d_rec, uint32_t *d_ext, uint32_t ext_cap,
+				      uint32_t *d_ext_count, uint64_t *d_counters, void *d_workspace,
+				      void *stream)
+{
+	if (n == 0)
+		return NSD_OK;
+	int rc = check_device_args(d_frames, d_desc, d_rec, d_ext, ext_cap, d_ext_count, d_counters, mode);
+	if (rc || !d_workspace)
+		return rc ? rc : NSD_ERR_ARG;
+	rc = nsd_launch_dissect_sll(d_frames, d_desc, d_sll, n, start_for(linktype), mode, d_rec, d_ext,
+				    ext_cap, d_ext_count, d_counters, d_workspace, 0, (hipStream_t)stream);
+	return rc ? NSD_ERR_HIP : NSD_OK;
+}
+
 extern "C" int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
 				     const nsd_desc_t *desc, uint32_t n, int linktype, int mode,
 				     nsd_rec *rec, uint32_t *ext, uint32_t ext_cap,
 				     uint32_t *ext_count, uint64_t *counters)
+{
+	return dissector_entry_batch_sll(frames, frames_len, desc, nullptr, n, linktype, mode, rec, ext,
+					 ext_cap, ext_count, counters);
+}
+
+extern "C" int dissector_entry_batch_sll(const uint8_t *frames, size_t frames_len,
+					 const nsd_desc_t *desc, const nsd_sll_t *sll, uint32_t n,
+					 int linktype, int mode, nsd_rec *rec, uint32_t *ext,
+					 uint32_t ext_cap, uint32_t *ext_count, uint64_t *counters)
 {
 	if (n == 0)
 		return NSD_OK;
@@ -242,17 +272,21 @@ extern "C" int dissector_entry_batch(const uint8_t *frames, size_t frames_len,
 		return NSD_ERR_HIP;
 	if (!grow(c.frames, c.frames_cap, frames_len + NSD_FRAME_PAD) || !grow(c.desc, c.desc_cap, n) ||
 	    !grow(c.rec, c.rec_cap, n) || (ext_cap && !grow(c.ext, c.ext_cap, ext_cap)) ||
-	    !grow(c.ws, c.ws_cap, nsd_launch_workspace_bytes(n)))
+	    !grow(c.ws, c.ws_cap, nsd_launch_workspace_bytes(n)) ||
+	    (sll && !grow(c.sll, c.sll_cap, (size_t)n * sizeof(nsd_sll_t))))
 		return NSD_ERR_NOMEM;
 	hipStream_t s = c.stream;
+	if (sll && !hip_ok(hipMemcpyAsync(c.sll, sll, (size_t)n * sizeof(nsd_sll_t), hipMemcpyHostToDevice, s),
+			   "H2D"))
+		return NSD_ERR_HIP;
 	bool ok = hip_ok(hipMemcpyAsync(c.frames, frames, frames_len, hipMemcpyHostToDevice, s), "H2D") &&
 		  hip_ok(hipMemsetAsync(c.frames + frames_len, 0, NSD_FRAME_PAD, s), "memset") &&
 		  hip_ok(hipMemcpyAsync(c.desc, desc, n * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D") &&
 		  hip_ok(hipMemsetAsync(c.ext_count, 0, 64 + NSD_NCOUNTERS * 8, s), "memset");
 	if (!ok)
 		return NSD_ERR_HIP;
-	if (nsd_launch_dissect(c.frames, c.desc, n, start_for(linktype), mode, c.rec,
-			       ext_cap ? c.ext : nullptr, ext_cap, c.ext_count, c.counters, c.ws, 0, s))
+	if (nsd_launch_dissect_sll(c.frames, c.desc, sll ? c.sll : nullptr, n, start_for(linktype), mode, c.rec,
+				   ext_cap ? c.ext : nullptr, ext_cap, c.ext_count, c.counters, c.ws, 0, s))
 		return NSD_ERR_HIP;
 	uint32_t used = 0;
 	ok = hip_ok(hipMemcpyAsync(rec, c.rec, n * sizeof(nsd_rec), hipMemcpyDeviceToHost, s), "D2H") &&
@@ -369,7 +403,6 @@ extern "C" void dissector_cleanup_all(void)
 extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype, int mode,
 				      struct sockaddr_ll *sll)
 {
-	(void)sll;
 	if (mode == PRINT_NONE)   // dissector.c:70-71
 		return;
 	if (len > NSD_MAX_CAPLEN) {
@@ -381,21 +414,25 @@ extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype,
 	nsd_rec rec;
 	uint32_t ext[NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS)];
 	uint32_t used = 0;
-	int rc = dissector_entry_batch(packet, len, &d, 1, linktype, pm, &rec, ext,
-				       NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS), &used, nullptr);
+	nsd_sll_t ll;
+	memset(&ll, 0, sizeof(ll));
+	if (sll)
+		memcpy(&ll, sll, sizeof(ll));   // struct sockaddr_ll is the same 20 bytes
+	int rc = dissector_entry_batch_sll(packet, len, &d, &ll, 1, linktype, pm, &rec, ext,
+					   NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS), &used, nullptr);
 	if (rc != NSD_OK) {
 		fprintf(stderr, "netsniff-dissect: device dissection failed (%d)\n", rc);
 		abort();   // like panic() (die.h:46): no CPU fallback
 	}
 	std::string s;
 	if (pm == PRINT_NORM || pm == PRINT_LESS) {
-		nsd::format_packet(s, packet, (uint32_t)len, linktype, pm, rec, ext);
+		nsd::format_packet(s, packet, (uint32_t)len, linktype, pm, rec, ext, &ll);
 		// post-chain dumps run on what the chain left (dissector.c:108-118):
 		// after print_full the exit op already pulled everything
 		if (pm == PRINT_LESS)
 			nsd::format_post_dump(s, packet, (uint32_t)len, mode, rec.data_off, rec.tail_off);
 	} else {
-		nsd::format_packet(s, packet, (uint32_t)len, linktype, mode, rec, ext);
+		nsd::format_packet(s, packet, (uint32_t)len, linktype, mode, rec, ext, &ll);
 	}
 	emit(s);
 }

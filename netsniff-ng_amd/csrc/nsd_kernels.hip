@@ -547,6 +547,32 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 	fc.flush(s_cnt, lane);
 }
 
+// The LINKTYPE_LINUX_SLL head (dissector_sll.c:39-82): pulls nothing; in
+// print_full the next ops come from the packet's sockaddr_ll: a hatype that
+// pcap_devtype_to_linktype (pcap_io.h:205-267) maps to LINKTYPE_EN10MB
+// continues in eth_lay2 with ntohs(sll_protocol) at offset 0, ARPHRD_NETLINK
+// continues with the netlink ops (a host leaf), anything else ends the chain
+// ("[ Unknown protocol ]").  print_less dispatches nothing.
+template <int MODE>
+__device__ __forceinline__ void sll_head(Shared &sh, WalkOut &w, const uint32_t *__restrict__ sll, uint32_t i)
+{
+	const uint32_t w0 = sll ? sll[5 * (size_t)i] : 0u;       // sll_family | sll_protocol << 16
+	const uint32_t w2 = sll ? sll[5 * (size_t)i + 2] : 0u;   // sll_hatype | pkttype << 16 | halen << 24
+	const uint32_t hatype = w2 & 0xFFFF;
+	const uint32_t proto = __builtin_bswap16((uint16_t)(w0 >> 16));
+	w.chain = NSD_OPS_SLL;
+	w.n = 1;
+	atomicAdd(&sh.cnt[NSD_CNT_OPS + NSD_OPS_SLL], 1ull);
+	int nx = 0;
+	if (MODE == PRINT_NORM) {
+		const bool eth = hatype == 1 || hatype == 768 || hatype == 769 || hatype == 772 || hatype == 776 ||
+				 hatype == 777 || hatype == 778 || hatype == 823;
+		const uint32_t e2 = sh.step[32 + NSD_L2H(proto)];
+		nx = eth ? ((e2 & 0xFFFF) == proto ? (int)(e2 >> 16) : 0) : hatype == 824 ? NSD_OPS_NLMSG : 0;
+	}
+	w.id = nx;
+}
+
 // The packets pass 1 queued (the block's own queue region), walked with the
 // resumable general walk.  Lanes are refilled: a lane whose chain ends takes
 // the next queued packet (entry and descriptor prefetched two rounds ahead),
@@ -560,7 +586,8 @@ __device__ __forceinline__ uint32_t pass2(Shared &sh, const uint8_t *__restrict_
 				      const uint64_t *__restrict__ desc, int start_id, uint4 *__restrict__ rec,
 				      const uint4 *__restrict__ queue, uint32_t region,
 				      uint64_t *__restrict__ pend2, uint32_t *__restrict__ ext, uint32_t ext_words,
-				      uint32_t *__restrict__ ext_used, uint32_t chunk, uint32_t q0)
+				      uint32_t *__restrict__ ext_used, uint32_t chunk, uint32_t q0,
+				      const uint32_t *__restrict__ sll)
 {
 	constexpr int ROW = row_of(WIN2);
 	const int lane = threadIdx.x & 63;
@@ -608,6 +635,8 @@ __device__ __forceinline__ uint32_t pass2(Shared &sh, const uint8_t *__restrict_
 						atomicAdd(&sh.cnt[NSD_CNT_OPS + ((w.chain >> (5 * k)) & 31)], 1ull);
 			} else {
 				walk_init(w, caplen, start_id);
+				if (start_id == NSD_OPS_SLL)
+					sll_head<MODE>(sh, w, sll, i);
 			}
 			wb = (w.data + m) & ~15u;
 			have = true;
@@ -808,7 +837,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	uint4 *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
 	uint4 *__restrict__ queue, uint32_t region, uint64_t *__restrict__ pend,
-	uint64_t *__restrict__ pend2)
+	uint64_t *__restrict__ pend2, const uint32_t *__restrict__ sll)
 {
 	__shared__ Shared sh;
 	if (threadIdx.x == 0) {
@@ -835,7 +864,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 			__syncthreads();   // the span's queue entries and sh.qn are complete
 #ifndef NSD_X_NOP2
 			q0 = pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, ext, ext_words,
-					 ext_used, chunk, q0);
+					 ext_used, chunk, q0, sll);
 #endif
 			__syncthreads();   // every wave is done taking entries: restart the taker at q0
 			if (threadIdx.x == 0)
@@ -880,10 +909,26 @@ extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 	return (16 + 8 + 8) * region_slots(n);
 }
 
+extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
+				      uint32_t n, int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
+				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
+				      void *d_ws, int grid, hipStream_t stream);
+
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
 				  int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
 				  uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
 				  void *d_ws, int grid, hipStream_t stream)
+{
+	return nsd_launch_dissect_sll(d_frames, d_desc, nullptr, n, start_id, mode, d_rec, d_ext, ext_words,
+				      d_ext_used, d_counters, d_ws, grid, stream);
+}
+
+// d_sll: one struct sockaddr_ll (nsd_sll_t, 20 bytes) per packet, or NULL
+// (read as zeros); used by the LINKTYPE_LINUX_SLL head only
+extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
+				      uint32_t n, int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
+				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
+				      void *d_ws, int grid, hipStream_t stream)
 {
 	using namespace nsd;
 	static int s_cus = 0;
@@ -932,6 +977,6 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 	hipLaunchKernelGGL(mi == 0 ? dissect_all<PRINT_NORM> : mi == 1 ? dissect_all<PRINT_LESS> : dissect_all<PRINT_HEX>,
 			   dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id,
 			   (uint4 *)d_rec, d_ext, ext_words, d_ext_used, chunk, (unsigned long long *)d_counters,
-			   queue, region, pend, pend2);
+			   queue, region, pend, pend2, (const uint32_t *)d_sll);
 	return hipGetLastError() == hipSuccess ? 0 : -2;
 }

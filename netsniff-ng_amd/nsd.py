@@ -68,7 +68,13 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_host_unregister", "nsd_bpf_validate", "nsd_bpf_load", "nsd_bpf_free",
                "nsd_bpf_workspace_bytes", "nsd_bpf_filter_device", "nsd_bpf_filter_batch",
                "nsd_pcap_open", "nsd_pcap_linktype", "nsd_pcap_read_batch", "nsd_pcap_close",
-               "nsd_replay_pcap", "nsd_t3_block_desc"]
+               "nsd_replay_pcap", "nsd_t3_block_desc", "nsd_dissect_device_sll",
+               "dissector_entry_batch_sll", "nsd_format_packet_sll"]
+
+# struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
+SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
+                      ("pkttype", "u1"), ("halen", "u1"), ("addr", "u1", (8,))])
+LINKTYPE_LINUX_SLL = 113
 
 _lib = None
 _vp, _u32, _u64, _int, _sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
@@ -152,6 +158,15 @@ def lib():
         L.nsd_pcap_read_batch.argtypes = [_vp, _vp, _sz, _vp, _u32, _vp, _vp]
         L.nsd_pcap_close.restype = None
         L.nsd_pcap_close.argtypes = [_vp]
+        L.dissector_entry_batch_sll.restype = _int
+        L.dissector_entry_batch_sll.argtypes = [_vp, _sz, _vp, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp]
+        L.nsd_dissect_device_sll.restype = _int
+        L.nsd_dissect_device_sll.argtypes = [_vp, _vp, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp,
+                                             _vp, _vp]
+        L.nsd_format_packet_sll.restype = ctypes.c_long
+        L.nsd_format_packet_sll.argtypes = [_vp, _u32, _int, _int, _vp, _vp, _vp, ctypes.c_char_p, _sz]
+        L.nsd_format_batch_sll.restype = ctypes.c_long
+        L.nsd_format_batch_sll.argtypes = [_vp, _vp, _vp, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]
         L.nsd_t3_block_desc.restype = ctypes.c_long
         L.nsd_t3_block_desc.argtypes = [_vp, _sz, _int, _int, _vp, _u32]
         L.nsd_replay_pcap.restype = ctypes.c_long
@@ -206,7 +221,7 @@ def dissect_device(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, rec=
     return rec, ext, ext_used, counters
 
 
-def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_words=None):
+def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_words=None, sll=None):
     """Host-memory batch through the device (H2D, kernel, D2H).
     Returns (rec, ext pool words[:used], counters) as numpy arrays."""
     frames = np.ascontiguousarray(frames, dtype=np.uint8)
@@ -218,9 +233,11 @@ def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_wor
     ext = np.zeros(max(ext_words, 1), dtype=np.uint32)
     used = np.zeros(1, dtype=np.uint32)
     counters = np.zeros(NCOUNTERS, dtype=np.uint64)
-    rc = lib().dissector_entry_batch(frames.ctypes.data, frames.nbytes, desc.ctypes.data, n,
-                                     linktype, mode, rec.ctypes.data, ext.ctypes.data, ext_words,
-                                     used.ctypes.data, counters.ctypes.data)
+    sll = None if sll is None else np.ascontiguousarray(sll, dtype=SLL_DTYPE)
+    rc = lib().dissector_entry_batch_sll(frames.ctypes.data, frames.nbytes, desc.ctypes.data,
+                                         None if sll is None else sll.ctypes.data, n,
+                                         linktype, mode, rec.ctypes.data, ext.ctypes.data, ext_words,
+                                         used.ctypes.data, counters.ctypes.data)
     _check(rc, "dissector_entry_batch")
     return rec, ext[:min(int(used[0]), ext_words)], counters
 
@@ -274,7 +291,7 @@ class Pipe:
         self.close()
 
 
-def format_batch(frames, desc, rec, ext=None, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB):
+def format_batch(frames, desc, rec, ext=None, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, sll=None):
     """Render records to the reference text (ext: the u32 pool the records'
     slots index).  Returns (list of bytes per packet, status array)."""
     n = len(desc)
@@ -287,9 +304,11 @@ def format_batch(frames, desc, rec, ext=None, mode=PRINT_NORM, linktype=LINKTYPE
     rc = np.zeros(n, dtype=np.int8)
     cap = int(frames.nbytes) * 7 + 1024 * n + 4096
     out = ctypes.create_string_buffer(cap)
-    total = lib().nsd_format_batch(frames.ctypes.data, desc.ctypes.data, n, linktype, mode,
-                                   rec.ctypes.data, ext_ptr, ctypes.addressof(out), cap,
-                                   ends.ctypes.data, rc.ctypes.data)
+    sll = None if sll is None else np.ascontiguousarray(sll, dtype=SLL_DTYPE)
+    total = lib().nsd_format_batch_sll(frames.ctypes.data, desc.ctypes.data,
+                                       None if sll is None else sll.ctypes.data, n, linktype, mode,
+                                       rec.ctypes.data, ext_ptr, ctypes.addressof(out), cap,
+                                       ends.ctypes.data, rc.ctypes.data)
     if total < 0:
         raise NsdError("format buffer too small")
     raw = out.raw[:total]

@@ -1267,6 +1267,115 @@ static int L_icmpv6(P *k, uint32_t layer_start)
 }
 
 /* run one ops' process() */
+/* ---- LINKTYPE_LINUX_SLL head (dissector_sll.c:17-82) ---------------------
+ * The packet's struct sockaddr_ll comes from nsor_set_sll (thread-local;
+ * NULL = zeros, like a zeroed pkt->sll). */
+static __thread const nsd_sll_t *g_sll;
+
+void nsor_set_sll(const nsd_sll_t *sll) { g_sll = sll; }
+
+static const char *sll_pkt_type2str(unsigned t)          /* dissector_sll.c:17-37 */
+{
+	switch (t) {
+	case 0: return "host";
+	case 1: return "broadcast";
+	case 2: return "multicast";
+	case 3: return "other host";
+	case 4: return "outgoing";
+	case 6: return "user";
+	case 7: return "kernel";
+	}
+	return "Unknown";
+}
+
+static const char *sll_device_type2str(unsigned t)       /* dev.c:252-402 */
+{
+	static const struct { unsigned t; const char *s; } tab[] = {
+		{1, "ether"}, {2, "eether"}, {3, "ax25"}, {4, "pronet"}, {5, "chaos"},
+		{6, "ieee802"}, {7, "arcnet"}, {8, "appletlk"}, {15, "dlci"}, {19, "atm"},
+		{23, "metricom"}, {24, "ieee1394"}, {32, "infiniband"}, {256, "slip"},
+		{257, "cslip"}, {258, "slip6"}, {259, "cslip6"}, {260, "RSRVD"}, {264, "adapt"},
+		{270, "rose"}, {271, "x25"}, {272, "hwx25"}, {280, "can"}, {512, "ppp"},
+		{513, "hdlc"}, {516, "lapb"}, {517, "ddcmp"}, {518, "rawhdlc"}, {768, "tunnel"},
+		{769, "tunnel6"}, {770, "frad"}, {771, "skip"}, {772, "loopback"},
+		{773, "localtlk"}, {774, "fddi"}, {775, "bif"}, {776, "sit"}, {777, "ipddp"},
+		{778, "ipgre"}, {779, "pimreg"}, {780, "hippi"}, {781, "ash"}, {782, "econet"},
+		{783, "irda"}, {784, "fcpp"}, {785, "fcal"}, {786, "fcpl"}, {787, "fcfb0"},
+		{788, "fcfb1"}, {789, "fcfb2"}, {790, "fcfb3"}, {791, "fcfb4"}, {792, "fcfb5"},
+		{793, "fcfb6"}, {794, "fcfb7"}, {795, "fcfb8"}, {796, "fcfb9"}, {797, "fcfb10"},
+		{798, "fcfb11"}, {799, "fcfb12"}, {800, "ieee802_tr"}, {801, "ieee80211"},
+		{802, "ieee80211_prism"}, {803, "ieee80211_radiotap"}, {804, "ieee802154"},
+		{820, "phonet"}, {821, "phonet_pipe"}, {822, "caif"}, {823, "ip6gre"},
+		{824, "netlink"}, {0xFFFE, "none"}, {0xFFFF, "void"},
+	};
+	for (size_t i = 0; i < sizeof(tab) / sizeof(tab[0]); i++)
+		if (tab[i].t == t)
+			return tab[i].s;
+	return "Unknown";
+}
+
+/* device_addr2str (dev.c:405-422) into sll_print_full's 40-byte buffer;
+ * bytes past sll_addr[8] read as zero (parity domain) */
+static void sll_device_addr2str(const uint8_t *addr8, int alen, int type, char *buf)
+{
+	uint8_t a[256];
+	memset(a, 0, sizeof(a));
+	memcpy(a, addr8, 8);
+	if (alen == 4 && (type == 768 || type == 776 || type == 778)) {
+		inet_ntop(AF_INET, a, buf, 40);
+		return;
+	}
+	if (alen == 16 && type == 769) {
+		inet_ntop(AF_INET6, a, buf, 40);
+		return;
+	}
+	snprintf(buf, 40, "%02x", a[0]);
+	for (int i = 1, l = 2; i < alen && l < 40; i++, l += 3)
+		snprintf(buf + l, 40 - l, ":%02x", a[i]);
+}
+
+static int L_sll(P *k)
+{
+	nsd_sll_t z;
+	const nsd_sll_t *s = g_sll;
+	char addr[64];
+	unsigned proto;
+	int cls;
+
+	if (!s) {
+		memset(&z, 0, sizeof(z));
+		s = &z;
+	}
+	proto = (unsigned)((s->protocol >> 8) | ((s->protocol & 0xFF) << 8));
+	memset(addr, 0, sizeof(addr));
+	sll_device_addr2str(s->addr, s->halen, s->hatype, addr);
+	if (k->mode == PRINT_NORM)
+		E(k, " [ Linux \"cooked\"");
+	E(k, " Pkt Type %d (%s)", s->pkttype, sll_pkt_type2str(s->pkttype));
+	E(k, ", If Type %d (%s)", s->hatype, sll_device_type2str(s->hatype));
+	E(k, ", Addr Len %d", s->halen);
+	E(k, ", Src (%s)", addr);
+	E(k, ", Proto 0x%x", proto);
+	if (k->mode != PRINT_NORM)
+		return 0;                    /* sll_print_less dispatches nothing */
+	E(k, " ]\n");
+	/* pcap_devtype_to_linktype (pcap_io.h:205-267) */
+	switch (s->hatype) {
+	case 768: case 769: case 772: case 776: case 777: case 778: case 823: case 1:
+		cls = 1; break;
+	case 824:
+		cls = 2; break;
+	default:
+		cls = 0;
+	}
+	if (cls == 1)
+		return lay2(proto);
+	if (cls == 2)
+		return NSD_OPS_NLMSG;
+	E(k, " [ Unknown protocol ]\n");
+	return 0;
+}
+
 static int run_layer(P *k, int id)
 {
 	uint32_t start = k->data;
@@ -1291,6 +1400,7 @@ static int run_layer(P *k, int id)
 	case NSD_OPS_UDP:            return L_udp(k);
 	case NSD_OPS_ICMPV4:         return L_icmp(k);
 	case NSD_OPS_ICMPV6:         return L_icmpv6(k, start);
+	case NSD_OPS_SLL:            return L_sll(k);
 	default:
 		/* ARP, LLDP, IGMP, DCCP (and non-Ethernet heads): host-rendered leaves */
 		k->host = 1;
@@ -1492,6 +1602,14 @@ uint64_t nsor_dissect_batch(const uint8_t *frames, const nsd_desc_t *desc, uint3
 			    int linktype, int mode, nsd_rec *rec, uint32_t *ext,
 			    uint32_t ext_words, uint32_t *ext_used, uint64_t *counters)
 {
+	return nsor_dissect_batch_sll(frames, desc, NULL, n, linktype, mode, rec, ext, ext_words,
+				      ext_used, counters);
+}
+
+uint64_t nsor_dissect_batch_sll(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+				uint32_t n, int linktype, int mode, nsd_rec *rec, uint32_t *ext,
+				uint32_t ext_words, uint32_t *ext_used, uint64_t *counters)
+{
 	uint64_t sw = 0;
 	nsor_info in;
 	nsd_rec r;
@@ -1499,6 +1617,7 @@ uint64_t nsor_dissect_batch(const uint8_t *frames, const nsd_desc_t *desc, uint3
 	for (uint32_t i = 0; i < n; i++) {
 		uint64_t d = desc[i];
 		uint32_t caplen = NSD_DESC_CAPLEN(d);
+		g_sll = sll ? sll + i : NULL;
 		nsor_dissect(frames + NSD_DESC_OFF(d), caplen, linktype, mode, NULL, &r, &in);
 		if ((r.nflags & 7) == NSD_N_EXT) {
 			/* dense pool entries in packet order (layout: netsniff_dissect.h) */
@@ -1530,6 +1649,7 @@ uint64_t nsor_dissect_batch(const uint8_t *frames, const nsd_desc_t *desc, uint3
 			count(counters, &r, &in, caplen);
 		sw += in.w_bytes;
 	}
+	g_sll = NULL;
 	return sw;
 }
 

@@ -50,6 +50,10 @@ typedef struct nsor_info {
 void nsor_dissect(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
 		  nsor_text *text, nsd_rec *rec, nsor_info *info);
 
+/* The struct sockaddr_ll the LINKTYPE_LINUX_SLL head prints and dispatches
+ * on, for the next nsor_dissect calls of this thread (NULL = zeros). */
+void nsor_set_sll(const nsd_sll_t *sll);
+
 /* Batch form producing exactly what the device produces.  Ext pool entries
  * are packed densely in packet order (the device hands them out in
  * arbitrary order from per-wave chunks; tests compare through the slot
@@ -58,6 +62,11 @@ void nsor_dissect(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
 uint64_t nsor_dissect_batch(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
 			    int linktype, int mode, nsd_rec *rec, uint32_t *ext,
 			    uint32_t ext_words, uint32_t *ext_used, uint64_t *counters);
+
+/* Same, with one struct sockaddr_ll per packet (SLL link types; may be NULL). */
+uint64_t nsor_dissect_batch_sll(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+				uint32_t n, int linktype, int mode, nsd_rec *rec, uint32_t *ext,
+				uint32_t ext_words, uint32_t *ext_used, uint64_t *counters);
 
 /* Same walk, text for every packet appended to *text (fields+text baseline). */
 uint64_t nsor_dissect_batch_text(const uint8_t *frames, const nsd_desc_t *desc,

@@ -47,6 +47,32 @@
 
 #include "nsd_oracle.h"
 
+/* dev.c (compiles from the reference as it lies): the tables the SLL head
+ * prints through (dissector_sll.c:48-51) */
+const char *device_type2str(uint16_t type);
+const char *device_addr2str(const unsigned char *addr, int alen, int type, char *buf, int blen);
+
+/* -T: dump device_type2str for every hatype that has a name, and
+ * device_addr2str for a fixed 8-byte address at every (alen, type) the
+ * formatter distinguishes, into a 40-byte buffer as sll_print_full does */
+static int dump_dev_tables(void)
+{
+	static const unsigned char addr[32] = { 0xde, 0xad, 0xbe, 0xef, 0x01, 0x02, 0x03, 0x04 };
+	static const int types[] = { 1, 768, 769, 776, 778, 772, 824, 0 };
+	char buf[40];
+	for (unsigned t = 0; t < 65536; t++) {
+		const char *s = device_type2str((uint16_t)t);
+		if (strcmp(s, "Unknown"))
+			printf("T %u %s\n", t, s);
+	}
+	for (size_t k = 0; k < sizeof(types) / sizeof(types[0]); k++)
+		for (int alen = 0; alen <= 8; alen++) {
+			memset(buf, 0, sizeof(buf));
+			printf("A %d %d %s\n", types[k], alen, device_addr2str(addr, alen, types[k], buf, sizeof(buf)));
+		}
+	return 0;
+}
+
 struct hash_table eth_lay2;
 struct hash_table eth_lay3;
 
@@ -230,6 +256,8 @@ int main(int argc, char **argv)
 	static char outbuf[1 << 20];
 
 	g_mode = PRINT_NORM;
+	if (argc > 1 && !strcmp(argv[1], "-T"))
+		return dump_dev_tables();
 	while ((opt = getopt(argc, argv, "m:nw:i:")) != -1) {
 		switch (opt) {
 		case 'm': g_mode = atoi(optarg); break;

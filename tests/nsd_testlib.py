@@ -135,6 +135,13 @@ def oracle():
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                            ctypes.c_void_p]
+        lib.nsor_dissect_batch_sll.restype = ctypes.c_uint64
+        lib.nsor_dissect_batch_sll.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.c_void_p, ctypes.c_void_p]
+        lib.nsor_set_sll.restype = None
+        lib.nsor_set_sll.argtypes = [ctypes.c_void_p]
         lib.nsor_dissect_batch_mt.restype = ctypes.c_uint64
         lib.nsor_dissect_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                               ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -152,7 +159,7 @@ def oracle():
     return _oracle
 
 
-def oracle_records(frames, desc, linktype=1, mode=PRINT_NORM, ext_words=None):
+def oracle_records(frames, desc, linktype=1, mode=PRINT_NORM, ext_words=None, sll=None):
     """Returns (rec, ext pool words[:used], counters, sum_w)."""
     lib = oracle()
     n = len(desc)
@@ -162,13 +169,14 @@ def oracle_records(frames, desc, linktype=1, mode=PRINT_NORM, ext_words=None):
     ext = np.zeros(max(ext_words, 1), dtype=np.uint32)
     used = np.zeros(1, dtype=np.uint32)
     counters = np.zeros(NCOUNTERS, dtype=np.uint64)
-    sw = lib.nsor_dissect_batch(frames.ctypes.data, desc.ctypes.data, n, linktype, mode,
-                                rec.ctypes.data, ext.ctypes.data, ext_words, used.ctypes.data,
-                                counters.ctypes.data)
+    sw = lib.nsor_dissect_batch_sll(frames.ctypes.data, desc.ctypes.data,
+                                    None if sll is None else sll.ctypes.data, n, linktype, mode,
+                                    rec.ctypes.data, ext.ctypes.data, ext_words, used.ctypes.data,
+                                    counters.ctypes.data)
     return rec, ext[:min(int(used[0]), ext_words)], counters, int(sw)
 
 
-def oracle_text_packets(frames, desc, linktype=1, mode=PRINT_NORM):
+def oracle_text_packets(frames, desc, linktype=1, mode=PRINT_NORM, sll=None):
     """Per-packet oracle text (list of (bytes, unsupported))."""
     lib = oracle()
     out = []
@@ -176,10 +184,12 @@ def oracle_text_packets(frames, desc, linktype=1, mode=PRINT_NORM):
     for i in range(len(desc)):
         t = _Text()
         p = frames[offs[i]:offs[i] + caps[i]]
+        lib.nsor_set_sll(None if sll is None else sll[i:i + 1].ctypes.data)
         lib.nsor_dissect(p.ctypes.data, int(caps[i]), linktype, mode, ctypes.byref(t), None, None)
         s = ctypes.string_at(t.buf, t.len) if t.len else b""
         out.append((s, bool(t.unsupported)))
         lib.nsor_text_free(ctypes.byref(t))
+    lib.nsor_set_sll(None)
     return out
 
 
