@@ -10,7 +10,7 @@ R=$(pwd)
 O=$R/gpurun_out/round
 mkdir -p "$O"
 fatal() { case $1 in 0) ;; *) echo "FATAL rc=$1 in $2"; exit $1;; esac; }
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > "$O/pytest_gpu.log" 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -n 3 "$O/pytest_gpu.log"; fatal $rc pytest
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -n 2 "$O/smoke.log"; fatal $rc smoke
