@@ -304,6 +304,16 @@ int dissector_entry_batch_sll(const uint8_t *frames, size_t frames_len,
 long nsd_format_packet_sll(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
 			   const nsd_rec *rec, const uint32_t *ext_pool, const nsd_sll_t *sll,
 			   char *out, size_t cap);
+/* nsd_format_batch_sll: packets [0, n) into one buffer (per-packet end
+ * offsets in ends[], status in rc[], both may be NULL); returns total bytes
+ * or -needed when cap is too small.  nsd_pipe_submit_sll: nsd_pipe_submit
+ * with one sockaddr_ll per packet (the pipe's link type is an SLL one). */
+long nsd_format_batch_sll(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+			  uint32_t n, int linktype, int mode, const nsd_rec *rec,
+			  const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends, int8_t *rc);
+int nsd_pipe_submit_sll(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
+			const nsd_desc_t *desc, const nsd_sll_t *sll, uint32_t n, nsd_rec *rec,
+			uint32_t *ext, uint32_t *ext_used, uint64_t *counters, int *status);
 
 /* ---- pcap replay front end (`netsniff-ng --in f.pcap`, read_pcap
  * netsniff-ng.c:640-770; pcap_io.h / pcap_sg.c record formats) ---------------
@@ -319,7 +329,8 @@ long nsd_format_packet_sll(const uint8_t *pkt, uint32_t caplen, int linktype, in
  * -EINVAL), or NSD_ERR_ARG.
  * nsd_replay_pcap: the whole replay loop: read -> optional device BPF filter
  * -> pipelined device walk -> formatter -> [tprintf wrap at `cols` > 0] ->
- * out_fd, in file order; counters (may be NULL) accumulates the counter
+ * out_fd, in file order (a *_LL file's cooked headers reach the SLL head as
+ * each packet's sockaddr_ll); counters (may be NULL) accumulates the counter
  * vector; `threads` host threads format each batch (<= 0: up to 16).
  * Returns the records printed or a negative NSD_ERR_*. */
 typedef struct nsd_pcap nsd_pcap;
@@ -328,6 +339,12 @@ nsd_pcap *nsd_pcap_open(const char *path);
 int nsd_pcap_linktype(const nsd_pcap *p);
 long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
 			 uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns);
+/* as nsd_pcap_read_batch, also filling sll[k] (may be NULL) as read_pcap
+ * fills fm.s_ll (netsniff-ng.c:672, 727; pcap_pkthdr_to_tpacket_hdr ->
+ * ll_to_sockaddr, pcap_io.h:182-191, 594-660): the *_LL record's cooked
+ * header, zeros for other record forms. */
+long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
+			     nsd_sll_t *sll, uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns);
 void nsd_pcap_close(nsd_pcap *p);
 long nsd_replay_pcap(const char *path, int mode, const struct nsd_bpf_prog *filter, int out_fd,
 		     int cols, uint64_t *counters, int threads);
@@ -344,6 +361,10 @@ long nsd_replay_pcap(const char *path, int mode, const struct nsd_bpf_prog *filt
  * inconsistent block or more than max_n frames. */
 long nsd_t3_block_desc(const uint8_t *block, size_t block_len, int packet_type, int lo_ifindex,
 		       nsd_desc_t *desc, uint32_t max_n);
+/* as nsd_t3_block_desc, also copying each kept frame's struct sockaddr_ll
+ * (hdr + 48) into sll[k] (may be NULL), for the SLL heads */
+long nsd_t3_block_desc_sll(const uint8_t *block, size_t block_len, int packet_type,
+			   int lo_ifindex, nsd_desc_t *desc, nsd_sll_t *sll, uint32_t max_n);
 
 /* ---- classic BPF on the device --------------------------------
  * The capture loop filters every record before dissecting it (read_pcap

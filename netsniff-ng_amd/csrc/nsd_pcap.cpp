@@ -32,10 +32,6 @@
 
 #include "../../include/netsniff_dissect.h"
 
-extern "C" long nsd_format_batch(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
-				 int linktype, int mode, const nsd_rec *rec, const uint32_t *ext_pool,
-				 char *out, size_t cap, uint64_t *ends, int8_t *rc);
-
 namespace {
 
 constexpr uint32_t TCPDUMP = 0xa1b2c3d4, NSEC = 0xa1b23c4d, KUZ = 0xa1b2cd34, BKM = 0xa1e2cb12;
@@ -152,6 +148,19 @@ extern "C" void nsd_pcap_close(nsd_pcap *p)
 extern "C" long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
 				    uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns)
 {
+	return nsd_pcap_read_batch_sll(p, frames, cap, desc, nullptr, max_n, wire_len, ts_ns);
+}
+
+// same, also filling sll[k] (may be NULL) the way read_pcap fills fm.s_ll
+// (netsniff-ng.c:672, 727): zeroed once, then for *_LL records
+// pcap_pkthdr_to_tpacket_hdr -> ll_to_sockaddr (pcap_io.h:182-191, 594-660)
+// from the cooked header after the record header (struct pcap_ll
+// {pkttype, hatype, len, addr[8], protocol}, every field big-endian in either
+// file byte order): pkttype / hatype / halen from be16, protocol kept as
+// stored (be16), addr copied; family and ifindex stay 0.
+extern "C" long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
+					nsd_sll_t *sll, uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns)
+{
 	if (!p || !frames || !desc || cap < NSD_FRAME_PAD)
 		return NSD_ERR_ARG;
 	size_t off = 0;
@@ -192,6 +201,19 @@ extern "C" long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, ns
 		memcpy(frames + at, h + p->hdrsize, caplen);
 		p->pos += p->hdrsize + caplen;
 		desc[n] = NSD_DESC(at, caplen);
+		if (sll) {
+			nsd_sll_t ll;
+			memset(&ll, 0, sizeof(ll));
+			if (p->ll_extra) {
+				const uint8_t *c = h + 16;   // struct pcap_ll
+				ll.pkttype = (uint8_t)(((uint32_t)c[0] << 8) | c[1]);
+				ll.hatype = (uint16_t)(((uint32_t)c[2] << 8) | c[3]);
+				ll.halen = (uint8_t)(((uint32_t)c[4] << 8) | c[5]);
+				memcpy(ll.addr, c + 6, 8);
+				memcpy(&ll.protocol, c + 14, 2);
+			}
+			sll[n] = ll;
+		}
 		if (wire_len)
 			wire_len[n] = wl;
 		if (ts_ns)
@@ -227,6 +249,7 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 	if (!p)
 		return NSD_ERR_ARG;
 	const int lt = (int)p->linktype;
+	const bool has_ll = p->ll_extra != 0;   // *_LL file: one sockaddr_ll per record
 	const uint32_t ext_words = 64 * BATCH;
 	nsd_pipe *pipe = nsd_pipe_create(BATCH, FRAME_BYTES, ext_words, DEPTH, lt, mode);
 	if (!pipe) {
@@ -236,6 +259,7 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 	struct Batch {
 		uint8_t *frames = nullptr;
 		nsd_desc_t *desc = nullptr;
+		nsd_sll_t *sll = nullptr;
 		nsd_rec *rec = nullptr;
 		uint32_t *ext = nullptr;
 		uint32_t *verdict = nullptr;
@@ -254,7 +278,9 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 		x.rec = (nsd_rec *)nsd_host_alloc(BATCH * sizeof(nsd_rec));
 		x.ext = (uint32_t *)nsd_host_alloc(ext_words * sizeof(uint32_t));
 		x.verdict = (uint32_t *)malloc(BATCH * sizeof(uint32_t));
-		if (!x.frames || !x.desc || !x.rec || !x.ext || !x.verdict)
+		if (has_ll)
+			x.sll = (nsd_sll_t *)nsd_host_alloc(BATCH * sizeof(nsd_sll_t));
+		if (!x.frames || !x.desc || !x.rec || !x.ext || !x.verdict || (has_ll && !x.sll))
 			rc = NSD_ERR_NOMEM;
 	}
 	// complete the oldest batch and print it
@@ -279,8 +305,9 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 			size_t cap = 256 * (size_t)(hi - lo) + 4096;
 			for (;;) {
 				part[t].resize(cap);
-				long r = nsd_format_batch(x.frames, x.desc + lo, hi - lo, lt, mode, x.rec + lo, x.ext,
-							  &part[t][0], cap, nullptr, nullptr);
+				long r = nsd_format_batch_sll(x.frames, x.desc + lo, x.sll ? x.sll + lo : nullptr,
+							      hi - lo, lt, mode, x.rec + lo, x.ext, &part[t][0],
+							      cap, nullptr, nullptr);
 				if (r >= 0) {
 					part[t].resize((size_t)r);
 					break;
@@ -328,7 +355,7 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 		Batch &x = b[slot];
 		if (x.busy && (rc = finish(x)) != NSD_OK)
 			break;
-		long n = nsd_pcap_read_batch(p, x.frames, FRAME_BYTES, x.desc, BATCH, nullptr, nullptr);
+		long n = nsd_pcap_read_batch_sll(p, x.frames, FRAME_BYTES, x.desc, x.sll, BATCH, nullptr, nullptr);
 		if (n < 0) {
 			rc = n;
 			break;
@@ -349,16 +376,19 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 			}
 			long m = 0;
 			for (long k = 0; k < n; k++)
-				if (x.verdict[k])
+				if (x.verdict[k]) {
+					if (x.sll)
+						x.sll[m] = x.sll[k];
 					x.desc[m++] = x.desc[k];
+				}
 			n = m;
 			if (n == 0)
 				continue;
 		}
 		x.n = (uint32_t)n;
 		memset(x.cnt, 0, sizeof(x.cnt));
-		int r = nsd_pipe_submit(pipe, x.frames, used, x.desc, x.n, x.rec, x.ext, &x.ext_used, x.cnt,
-					&x.status);
+		int r = nsd_pipe_submit_sll(pipe, x.frames, used, x.desc, x.sll, x.n, x.rec, x.ext, &x.ext_used,
+					    x.cnt, &x.status);
 		if (r != NSD_OK) {
 			rc = r;
 			break;
@@ -378,6 +408,7 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 	for (auto &x : b) {
 		nsd_host_free(x.frames);
 		nsd_host_free(x.desc);
+		nsd_host_free(x.sll);
 		nsd_host_free(x.rec);
 		nsd_host_free(x.ext);
 		free(x.verdict);
@@ -404,6 +435,15 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 extern "C" long nsd_t3_block_desc(const uint8_t *block, size_t block_len, int packet_type,
 				  int lo_ifindex, nsd_desc_t *desc, uint32_t max_n)
 {
+	return nsd_t3_block_desc_sll(block, block_len, packet_type, lo_ifindex, desc, nullptr, max_n);
+}
+
+// same, also copying each kept frame's sockaddr_ll (hdr + 48, the `sll`
+// walk_t3_block hands to dissector_entry_point, netsniff-ng.c:1011-1025)
+// into sll[k] (may be NULL): the per-packet input of the SLL heads
+extern "C" long nsd_t3_block_desc_sll(const uint8_t *block, size_t block_len, int packet_type,
+				      int lo_ifindex, nsd_desc_t *desc, nsd_sll_t *sll, uint32_t max_n)
+{
 	if (!block || !desc || block_len < 48)
 		return NSD_ERR_ARG;
 	uint32_t num_pkts, first;
@@ -427,6 +467,8 @@ extern "C" long nsd_t3_block_desc(const uint8_t *block, size_t block_len, int pa
 		if (!skip) {
 			if (h + mac + (size_t)snaplen > block_len || snaplen > NSD_MAX_CAPLEN || n >= max_n)
 				return NSD_ERR_ARG;
+			if (sll)
+				memcpy(&sll[n], block + h + 48, sizeof(nsd_sll_t));
 			desc[n++] = NSD_DESC(h + mac, snaplen);
 		}
 		if (i + 1 < num_pkts) {

@@ -11,10 +11,10 @@
 
 #include "../../include/netsniff_dissect.h"
 
-extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
-				  int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
-				  uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
-				  void *d_ws, int grid, hipStream_t stream);
+extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
+				      uint32_t n, int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
+				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
+				      void *d_ws, int grid, hipStream_t stream);
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
 int nsd_start_for(int linktype);
 
@@ -35,6 +35,7 @@ struct Slot {
 	hipEvent_t done = nullptr;
 	uint8_t *frames = nullptr;
 	uint64_t *desc = nullptr;
+	nsd_sll_t *sll = nullptr;    // per-packet sockaddr_ll (SLL link types)
 	nsd_rec *rec = nullptr;
 	uint32_t *ext = nullptr;
 	uint32_t *small = nullptr;   // ext_count at +0, counters at +64 (device)
@@ -69,6 +70,7 @@ static void slot_free(Slot &s)
 	if (s.done) (void)hipEventDestroy(s.done);
 	if (s.frames) (void)hipFree(s.frames);
 	if (s.desc) (void)hipFree(s.desc);
+	if (s.sll) (void)hipFree(s.sll);
 	if (s.rec) (void)hipFree(s.rec);
 	if (s.ext) (void)hipFree(s.ext);
 	if (s.small) (void)hipFree(s.small);
@@ -109,6 +111,7 @@ extern "C" nsd_pipe *nsd_pipe_create(uint32_t max_pkts, size_t max_frame_bytes, 
 			    ok(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "event") &&
 			    ok(hipMalloc(&s.frames, max_frame_bytes + NSD_FRAME_PAD), "hipMalloc") &&
 			    ok(hipMalloc(&s.desc, (size_t)max_pkts * 8), "hipMalloc") &&
+			    ok(hipMalloc(&s.sll, (size_t)max_pkts * sizeof(nsd_sll_t)), "hipMalloc") &&
 			    ok(hipMalloc(&s.rec, (size_t)max_pkts * sizeof(nsd_rec)), "hipMalloc") &&
 			    (!ext_cap || ok(hipMalloc(&s.ext, (size_t)ext_cap * 4), "hipMalloc")) &&
 			    ok(hipMalloc(&s.small, 64 + NSD_NCOUNTERS * 8), "hipMalloc") &&
@@ -177,6 +180,17 @@ extern "C" int nsd_pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames
 			       const nsd_desc_t *desc, uint32_t n, nsd_rec *rec, uint32_t *ext,
 			       uint32_t *ext_count, uint64_t *counters, int *status)
 {
+	return nsd_pipe_submit_sll(p, frames, frames_len, desc, nullptr, n, rec, ext, ext_count, counters,
+				   status);
+}
+
+// same, with one sockaddr_ll per packet (pkt->sll of the SLL heads; the
+// *_LL pcap record's cooked header or the RX ring's per-frame sockaddr_ll);
+// sll may be NULL (the heads read zeros)
+extern "C" int nsd_pipe_submit_sll(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
+				   const nsd_desc_t *desc, const nsd_sll_t *sll, uint32_t n, nsd_rec *rec,
+				   uint32_t *ext, uint32_t *ext_count, uint64_t *counters, int *status)
+{
 	if (!p || (n && (!frames || !desc || !rec)) || (p->ext_cap && !ext && n))
 		return NSD_ERR_ARG;
 	if (n > p->max_pkts || frames_len > p->max_bytes)
@@ -205,10 +219,13 @@ extern "C" int nsd_pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames
 	if (good && n) {
 		good = ok(hipMemcpyAsync(s.frames, frames, frames_len, hipMemcpyHostToDevice, st), "H2D") &&
 		       ok(hipMemsetAsync(s.frames + frames_len, 0, NSD_FRAME_PAD, st), "memset") &&
-		       ok(hipMemcpyAsync(s.desc, desc, (size_t)n * 8, hipMemcpyHostToDevice, st), "H2D");
-		good = good && nsd_launch_dissect(s.frames, s.desc, n, p->start_id, p->mode, s.rec,
-						  p->ext_cap ? s.ext : nullptr, p->ext_cap, s.small,
-						  (uint64_t *)((uint8_t *)s.small + 64), s.ws, 0, st) == 0;
+		       ok(hipMemcpyAsync(s.desc, desc, (size_t)n * 8, hipMemcpyHostToDevice, st), "H2D") &&
+		       (!sll || ok(hipMemcpyAsync(s.sll, sll, (size_t)n * sizeof(nsd_sll_t), hipMemcpyHostToDevice,
+						  st), "H2D"));
+		good = good && nsd_launch_dissect_sll(s.frames, s.desc, sll ? s.sll : nullptr, n, p->start_id,
+						      p->mode, s.rec, p->ext_cap ? s.ext : nullptr, p->ext_cap,
+						      s.small, (uint64_t *)((uint8_t *)s.small + 64), s.ws, 0,
+						      st) == 0;
 		good = good && ok(hipMemcpyAsync(rec, s.rec, (size_t)n * sizeof(nsd_rec), hipMemcpyDeviceToHost,
 						 st), "D2H");
 	}

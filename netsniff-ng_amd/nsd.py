@@ -69,7 +69,8 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_bpf_workspace_bytes", "nsd_bpf_filter_device", "nsd_bpf_filter_batch",
                "nsd_pcap_open", "nsd_pcap_linktype", "nsd_pcap_read_batch", "nsd_pcap_close",
                "nsd_replay_pcap", "nsd_t3_block_desc", "nsd_dissect_device_sll",
-               "dissector_entry_batch_sll", "nsd_format_packet_sll"]
+               "dissector_entry_batch_sll", "nsd_format_packet_sll", "nsd_format_batch_sll",
+               "nsd_pipe_submit_sll", "nsd_pcap_read_batch_sll", "nsd_t3_block_desc_sll"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -169,6 +170,12 @@ def lib():
         L.nsd_format_batch_sll.argtypes = [_vp, _vp, _vp, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]
         L.nsd_t3_block_desc.restype = ctypes.c_long
         L.nsd_t3_block_desc.argtypes = [_vp, _sz, _int, _int, _vp, _u32]
+        L.nsd_t3_block_desc_sll.restype = ctypes.c_long
+        L.nsd_t3_block_desc_sll.argtypes = [_vp, _sz, _int, _int, _vp, _vp, _u32]
+        L.nsd_pcap_read_batch_sll.restype = ctypes.c_long
+        L.nsd_pcap_read_batch_sll.argtypes = [_vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp]
+        L.nsd_pipe_submit_sll.restype = _int
+        L.nsd_pipe_submit_sll.argtypes = [_vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
         L.nsd_replay_pcap.restype = ctypes.c_long
         L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp, _int]
         _lib = L
@@ -257,17 +264,21 @@ class Pipe:
         self.depth = depth
         self.inflight = []
 
-    def submit(self, frames, desc, rec, ext=None, ext_used=None, counters=None, status=None):
-        """ext: u32[ext_words] receiving the pool, ext_used: u32[1]."""
+    def submit(self, frames, desc, rec, ext=None, ext_used=None, counters=None, status=None, sll=None):
+        """ext: u32[ext_words] receiving the pool, ext_used: u32[1]; sll: one
+        SLL_DTYPE sockaddr_ll per packet (SLL link types) or None."""
         n = len(desc)
         ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
         if ext is not None:
             assert ext.dtype == np.uint32 and len(ext) >= self.ext_words
-        rc = self.L.nsd_pipe_submit(self.p, frames.ctypes.data, frames.nbytes, desc.ctypes.data, n,
-                                    rec.ctypes.data, ptr(ext), ptr(ext_used), ptr(counters),
-                                    ptr(status))
-        _check(rc, "nsd_pipe_submit")
-        self.inflight.append((frames, desc, rec, ext, ext_used, counters, status))
+        if sll is not None:
+            sll = np.ascontiguousarray(sll, dtype=SLL_DTYPE)
+            assert len(sll) == n
+        rc = self.L.nsd_pipe_submit_sll(self.p, frames.ctypes.data, frames.nbytes, desc.ctypes.data,
+                                        ptr(sll), n, rec.ctypes.data, ptr(ext), ptr(ext_used),
+                                        ptr(counters), ptr(status))
+        _check(rc, "nsd_pipe_submit_sll")
+        self.inflight.append((frames, desc, rec, ext, ext_used, counters, status, sll))
         if len(self.inflight) > self.depth:   # the library completed the oldest first
             self.inflight.pop(0)
 
@@ -415,9 +426,10 @@ class BpfProgram:
 
 
 # ---- pcap replay front end (nsd_pcap.cpp) ---------------------------------------
-def pcap_read(path, cap=64 << 20, max_n=1 << 16):
-    """Read a whole pcap through nsd_pcap_read_batch: (linktype, [batches]),
-    each batch = (frames uint8, desc uint64, wire_len uint32, ts_ns uint64)."""
+def pcap_read(path, cap=64 << 20, max_n=1 << 16, sll=False):
+    """Read a whole pcap through nsd_pcap_read_batch_sll: (linktype, [batches]),
+    each batch = (frames uint8, desc uint64, wire_len uint32, ts_ns uint64)
+    [+ one SLL_DTYPE sockaddr_ll per record when sll=True]."""
     L = lib()
     h = L.nsd_pcap_open(os.fsencode(path))
     if not h:
@@ -430,13 +442,15 @@ def pcap_read(path, cap=64 << 20, max_n=1 << 16):
             desc = np.zeros(max_n, dtype=np.uint64)
             wl = np.zeros(max_n, dtype=np.uint32)
             ts = np.zeros(max_n, dtype=np.uint64)
-            n = L.nsd_pcap_read_batch(h, frames.ctypes.data, cap, desc.ctypes.data, max_n,
-                                      wl.ctypes.data, ts.ctypes.data)
+            ll = np.zeros(max_n, dtype=SLL_DTYPE)
+            n = L.nsd_pcap_read_batch_sll(h, frames.ctypes.data, cap, desc.ctypes.data,
+                                          ll.ctypes.data if sll else None, max_n,
+                                          wl.ctypes.data, ts.ctypes.data)
             if n < 0:
                 raise NsdError(f"nsd_pcap_read_batch failed with status {n}")
             if n == 0:
                 return lt, out
-            out.append((frames, desc[:n], wl[:n], ts[:n]))
+            out.append((frames, desc[:n], wl[:n], ts[:n]) + ((ll[:n],) if sll else ()))
     finally:
         L.nsd_pcap_close(h)
 
@@ -461,11 +475,13 @@ def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None, threads
         return n, f.read()
 
 
-def t3_block_desc(block, packet_type=-1, lo_ifindex=-1, max_n=1 << 16):
-    """Descriptors of a TPACKET_V3 block's frames (nsd_t3_block_desc)."""
+def t3_block_desc(block, packet_type=-1, lo_ifindex=-1, max_n=1 << 16, sll=False):
+    """Descriptors of a TPACKET_V3 block's frames (nsd_t3_block_desc_sll);
+    with sll=True also each kept frame's sockaddr_ll: (desc, sll)."""
     block = np.ascontiguousarray(block, dtype=np.uint8)
     desc = np.zeros(max_n, dtype=np.uint64)
-    n = lib().nsd_t3_block_desc(block.ctypes.data, block.nbytes, packet_type, lo_ifindex,
-                                desc.ctypes.data, max_n)
-    _check(0 if n >= 0 else n, "nsd_t3_block_desc")
-    return desc[:n]
+    ll = np.zeros(max_n, dtype=SLL_DTYPE)
+    n = lib().nsd_t3_block_desc_sll(block.ctypes.data, block.nbytes, packet_type, lo_ifindex,
+                                    desc.ctypes.data, ll.ctypes.data if sll else None, max_n)
+    _check(0 if n >= 0 else n, "nsd_t3_block_desc_sll")
+    return (desc[:n], ll[:n]) if sll else desc[:n]

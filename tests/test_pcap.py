@@ -182,3 +182,82 @@ def test_replay_prefix_digest(tmp_path, key, cfg, mode):
     n, text = nsd.replay_pcap(path, mode=mode, threads=8)
     assert n == 65536
     assert hashlib.sha256(text).hexdigest() == want
+
+
+def write_ll_pcap(path, pkts, slls, endian="<", magic=0xA1B2C3D4):
+    """A LINKTYPE_LINUX_SLL file: each record = pcap_pkthdr + struct pcap_ll
+    (pkttype, hatype, len, addr[8], protocol; big-endian fields,
+    pcap_io.h:63-69, 171-180 sockaddr_to_ll) + the packet."""
+    with open(path, "wb") as f:
+        f.write(struct.pack(endian + "IHHiIII", magic, 2, 4, 0, 0, 65535, 113))
+        for i, (p, s) in enumerate(zip(pkts, slls)):
+            ll = struct.pack(">HHH8s", int(s["pkttype"]), int(s["hatype"]), int(s["halen"]),
+                             bytes(s["addr"])) + struct.pack(">H", int(s["protocol"]))
+            f.write(struct.pack(endian + "IIII", 1000 + i, i, len(p) + 16, len(p) + 16))
+            f.write(ll + bytes(p))
+
+
+def as_read(slls):
+    """The sockaddr_ll read_pcap hands the dissector for those records:
+    ll_to_sockaddr fills pkttype / hatype / halen / protocol / addr; family
+    and ifindex stay as memset (netsniff-ng.c:672)."""
+    r = np.zeros(len(slls), dtype=nsd.SLL_DTYPE)
+    for f in ("protocol", "hatype", "pkttype", "halen", "addr"):
+        r[f] = slls[f]
+    return r
+
+
+@pytest.mark.parametrize("endian", ["<", ">"])
+def test_reader_sll_cooked_headers(tmp_path, endian):
+    import test_sll as TS
+    cases = TS.sll_cases()
+    pkts = [p for p, _ in cases]
+    slls = np.array([s for _, s in cases], dtype=nsd.SLL_DTYPE)
+    path = str(tmp_path / "ll.pcap")
+    write_ll_pcap(path, pkts, slls, endian=endian)
+    lt, batches = nsd.pcap_read(path, sll=True, max_n=50)
+    assert len(batches) > 1
+    got = np.concatenate([b[4] for b in batches]).astype(nsd.SLL_DTYPE)   # concatenate canonicalises byte order
+    assert got.tobytes() == as_read(slls).tobytes()
+    got_pkts = []
+    for b in batches:
+        for d in b[1]:
+            d = int(d)
+            got_pkts.append(bytes(b[0][d & 0xFFFFFFFFFF:(d & 0xFFFFFFFFFF) + (d >> 40)]))
+    assert got_pkts == pkts
+    # other record forms: zeros (fm.s_ll as memset)
+    plain = str(tmp_path / "plain.pcap")
+    T.write_pcap(plain, pkts[:9])
+    _, b2 = nsd.pcap_read(plain, sll=True)
+    assert not b2[0][4].tobytes().strip(b"\0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_replay_sll_file(tmp_path, mode):
+    """`--in` an SLL capture: each record's cooked header reaches the SLL
+    head as its sockaddr_ll; the text equals the restatement's per packet
+    (netlink-continued packets left out: nlmsg is outside the path)."""
+    import test_sll as TS
+    cases = [c for c in TS.sll_cases() if int(c[1]["hatype"]) != 824]
+    pkts = [p for p, _ in cases]
+    slls = np.array([s for _, s in cases], dtype=nsd.SLL_DTYPE)
+    path = str(tmp_path / "ll.pcap")
+    write_ll_pcap(path, pkts, slls)
+    frames, desc = T.batch_from_packets(pkts)
+    ora = T.oracle_text_packets(frames, desc, linktype=nsd.LINKTYPE_LINUX_SLL, mode=mode, sll=as_read(slls))
+    orec, oext, ocnt, _ = T.oracle_records(frames, desc, linktype=nsd.LINKTYPE_LINUX_SLL, mode=mode,
+                                           sll=as_read(slls))
+    # leaves the restatement does not render as text (ARP / LLDP bodies):
+    # the product renderer's text over the oracle's records (pinned against
+    # the reference objects in test_golden / test_sll)
+    fmt, rc = nsd.format_batch(frames, desc, orec, oext, mode=mode, linktype=nsd.LINKTYPE_LINUX_SLL,
+                               sll=as_read(slls))
+    assert not any(rc)
+    want = b"".join(fmt[i] if u else t for i, (t, u) in enumerate(ora))
+    assert sum(u for _, u in ora) < len(ora) // 2
+    cnt = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
+    n, text = nsd.replay_pcap(path, mode=mode, counters=cnt)
+    assert n == len(pkts)
+    assert text == want
+    assert np.array_equal(cnt, ocnt)

@@ -15,7 +15,7 @@ import nsd_testlib as T
 PACKET_HOST, PACKET_OUTGOING = 0, 4
 
 
-def make_block(pkts, pkttypes=None, ifindex=None, block_len=1 << 20, mac_pad=2):
+def make_block(pkts, pkttypes=None, ifindex=None, block_len=1 << 20, mac_pad=2, slls=None):
     """tpacket_block_desc (48 B) + per frame tpacket3_hdr (48 B) + sockaddr_ll
     (20 B) + pad so the MAC header sits at 2 mod 16 (as the kernel places it),
     frames TPACKET_ALIGN'ed (16)."""
@@ -31,7 +31,7 @@ def make_block(pkts, pkttypes=None, ifindex=None, block_len=1 << 20, mac_pad=2):
         blk[h:h + len(hdr)] = hdr
         pt = pkttypes[i] if pkttypes else PACKET_HOST
         ix = ifindex[i] if ifindex else 2
-        sll = struct.pack("<HHiHBB8s", 17, 0x0008, ix, 1, pt, 6, bytes(8))
+        sll = struct.pack("<HHiHBB8s", 17, 0x0008, ix, 1, pt, 6, bytes(8)) if slls is None else slls[i].tobytes()
         blk[h + 48:h + 48 + 20] = sll
         blk[h + mac:h + mac + len(p)] = p
         offs.append(h + mac)
@@ -83,4 +83,48 @@ def test_block_dissect_on_device(mode):
     rec, ext, cnt = nsd.entry_batch(blk, desc, mode=mode)
     orec, oext, ocnt, _ = T.oracle_records(blk, desc, mode=mode)
     assert_same_records(rec, orec, ext, oext)
+    assert np.array_equal(cnt, ocnt)
+
+
+def test_block_sll_copied():
+    """nsd_t3_block_desc_sll hands each kept frame's sockaddr_ll (hdr + 48,
+    walk_t3_block's `sll`) out beside its descriptor, skip rules applied."""
+    pkts = [p for p in edge_cases.cases() if p][:30]
+    types = [PACKET_OUTGOING if i % 3 == 0 else PACKET_HOST for i in range(30)]
+    ifx = [1 if i % 2 == 0 else 2 + i for i in range(30)]
+    blk, offs = make_block(pkts, types, ifx)
+    desc, sll = nsd.t3_block_desc(blk, packet_type=-1, lo_ifindex=1, sll=True)
+    keep = [i for i in range(30) if not (ifx[i] == 1 and types[i] == 4)]
+    assert [int(x) & 0xFFFFFFFFFF for x in desc] == [offs[i] for i in keep]
+    assert list(sll["ifindex"]) == [ifx[i] for i in keep]
+    assert list(sll["pkttype"]) == [types[i] for i in keep]
+    assert set(sll["protocol"]) == {0x0800} and set(sll["hatype"]) == {1} and set(sll["family"]) == {17}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_cooked_ring_through_pipe(mode):
+    """A cooked (LINKTYPE_LINUX_SLL) ring: the block is the frame buffer, the
+    per-frame sockaddr_ll goes with it through nsd_pipe_submit_sll, records
+    and counters equal the oracle's."""
+    from test_device_parity import assert_same_records
+    import test_sll as TS
+    cases = TS.sll_cases()
+    slls = np.array([s for _, s in cases], dtype=nsd.SLL_DTYPE)
+    blk, _ = make_block([p for p, _ in cases], slls=slls)
+    desc, sll = nsd.t3_block_desc(blk, sll=True)
+    assert sll.tobytes() == slls.tobytes()
+    n = len(desc)
+    words = nsd.ext_pool_words(n)
+    pipe = nsd.Pipe(n, blk.nbytes, ext_words=words, depth=2, mode=mode, linktype=nsd.LINKTYPE_LINUX_SLL)
+    rec = np.zeros(n, dtype=nsd.REC_DTYPE)
+    ext = np.zeros(words, dtype=np.uint32)
+    used = np.zeros(1, dtype=np.uint32)
+    cnt = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
+    st = np.full(1, -99, dtype=np.int32)
+    pipe.submit(blk, desc, rec, ext, used, cnt, st, sll=sll)
+    assert pipe.drain() == 0 and st[0] == 0
+    pipe.close()
+    orec, oext, ocnt, _ = T.oracle_records(blk, desc, linktype=nsd.LINKTYPE_LINUX_SLL, mode=mode, sll=sll)
+    assert_same_records(rec, orec, ext[:int(used[0])], oext)
     assert np.array_equal(cnt, ocnt)
