@@ -48,6 +48,9 @@ constexpr int row_of(int W) { return W / 4 + 1; }
 #ifndef NSD_P1_TILES
 #define NSD_P1_TILES 16            // pass-1 grid strides per pass-2 round (0: whole shard)
 #endif
+#ifndef NSD_P2_WAVES
+#define NSD_P2_WAVES 4             // waves of a block that walk its pass-2 queue
+#endif
 #ifndef NSD_CSUM_SPLIT
 #define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
 #endif
@@ -863,8 +866,11 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 		if (MODE == PRINT_NORM || MODE == PRINT_LESS) {
 			__syncthreads();   // the span's queue entries and sh.qn are complete
 #ifndef NSD_X_NOP2
-			q0 = pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, ext, ext_words,
-					 ext_used, chunk, q0, sll);
+			// (waves take queue entries dynamically and pass 2 has no block
+			// barrier, so fewer walkers only changes who drains the queue)
+			if ((threadIdx.x >> 6) < NSD_P2_WAVES)
+				q0 = pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, ext,
+						 ext_words, ext_used, chunk, q0, sll);
 #endif
 			__syncthreads();   // every wave is done taking entries: restart the taker at q0
 			if (threadIdx.x == 0)
