@@ -353,7 +353,8 @@ def test_device_random_programs():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,n", [(T.SYN_IMIX, 100000), (T.SYN_UDP64, 3000), (T.SYN_IPV6X, 1)])
+@pytest.mark.parametrize("cfg,n", [(T.SYN_IMIX, 100000), (T.SYN_UDP64, 3000), (T.SYN_IPV6X, 1),
+                                   (T.SYN_IMIX, 1024), (T.SYN_IMIX, 1025), (T.SYN_IMIX, 3 << 20)])
 def test_device_compaction(cfg, n):
     """Device-resident filter with compaction: verdicts identical to the
     oracle's, the accepted descriptors packed in batch order."""
