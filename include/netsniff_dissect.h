@@ -348,6 +348,13 @@ long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_
 void nsd_pcap_close(nsd_pcap *p);
 long nsd_replay_pcap(const char *path, int mode, const struct nsd_bpf_prog *filter, int out_fd,
 		     int cols, uint64_t *counters, int threads);
+/* nsd_replay_pcap plus `--out f.pcap` (read_pcap netsniff-ng.c:636, 693-697,
+ * 739-746): with pcap_fd >= 0 writes the file header pcap_generic_push_fhdr
+ * writes for the replayed file's magic / link type, then every record that
+ * passed the filter exactly as read (record header, *_LL cooked header,
+ * bytes), in file order; pcap_fd < 0 is nsd_replay_pcap. */
+long nsd_replay_pcap_out(const char *path, int mode, const struct nsd_bpf_prog *filter, int out_fd,
+			 int cols, uint64_t *counters, int threads, int pcap_fd);
 
 /* ---- TPACKET_V3 RX ring front end (walk_t3_block, netsniff-ng.c:990-1039) --
  * nsd_t3_block_desc: descriptors for the frames of one retired ring block

@@ -49,6 +49,7 @@ struct nsd_pcap {
 	uint32_t hdrsize = 16;   // record header bytes (pcap_get_hdr_length)
 	uint32_t ll_extra = 0;   // cooked-header bytes counted in caplen (*_LL)
 	uint32_t linktype = 0;   // as stored in the file header
+	uint32_t magic_raw = 0;  // as stored in the file header
 	bool nsec = false;
 	bool eof = false;
 	// buffered reader (the scatter-gather reader's iovecs, pcap_sg.c)
@@ -102,6 +103,7 @@ extern "C" nsd_pcap *nsd_pcap_open(const char *path)
 	memcpy(&vmaj, h + 4, 2);
 	memcpy(&vmin, h + 6, 2);
 	// pcap_check_magic (pcap_io.h:286-320)
+	p->magic_raw = magic;
 	uint32_t m = magic;
 	if (m == bswap32(TCPDUMP) || m == bswap32(NSEC) || m == bswap32(KUZ) || m == bswap32(BKM)) {
 		p->swapped = true;
@@ -158,8 +160,19 @@ extern "C" long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, ns
 // {pkttype, hatype, len, addr[8], protocol}, every field big-endian in either
 // file byte order): pkttype / hatype / halen from be16, protocol kept as
 // stored (be16), addr copied; family and ifindex stay 0.
+static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc, nsd_sll_t *sll,
+		       uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns, uint8_t *rhdr);
+
 extern "C" long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
 					nsd_sll_t *sll, uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns)
+{
+	return read_batch(p, frames, cap, desc, sll, max_n, wire_len, ts_ns, nullptr);
+}
+
+// rhdr (may be NULL): each record's header bytes as stored (hdrsize <= 32,
+// 32-byte stride), for the pcap write-out
+static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc, nsd_sll_t *sll,
+		       uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns, uint8_t *rhdr)
 {
 	if (!p || !frames || !desc || cap < NSD_FRAME_PAD)
 		return NSD_ERR_ARG;
@@ -201,6 +214,8 @@ extern "C" long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap
 		memcpy(frames + at, h + p->hdrsize, caplen);
 		p->pos += p->hdrsize + caplen;
 		desc[n] = NSD_DESC(at, caplen);
+		if (rhdr)
+			memcpy(rhdr + 32 * (size_t)n, h, p->hdrsize);
 		if (sll) {
 			nsd_sll_t ll;
 			memset(&ll, 0, sizeof(ll));
@@ -236,6 +251,55 @@ extern "C" long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap
 extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *filter, int out_fd,
 				int cols, uint64_t *counters, int threads)
 {
+	return nsd_replay_pcap_out(path, mode, filter, out_fd, cols, counters, threads, -1);
+}
+
+static bool write_all(int fd, const void *buf, size_t n)
+{
+	const uint8_t *w = (const uint8_t *)buf;
+	while (n) {
+		ssize_t r = write(fd, w, n);
+		if (r < 0 && errno == EINTR)
+			continue;
+		if (r <= 0)
+			return false;
+		w += r;
+		n -= (size_t)r;
+	}
+	return true;
+}
+
+// pcap_generic_push_fhdr -> pcap_prepare_header (pcap_io.h:813-843, 936-950)
+// with the replayed file's magic and link type as read_pcap holds them
+// (ctx->magic / ctx->link_type, netsniff-ng.c:694-695): the *_LL remap undone
+// (the stored magic), version 2.4, thiszone 0, sigfigs 0, snaplen 65535,
+// link type swapped once more when the magic is a swapped one (as the
+// reference does with the as-stored value)
+static bool push_fhdr(const nsd_pcap *p, int fd)
+{
+	uint8_t h[24];
+	const bool sw = p->swapped;
+	const uint16_t vmaj = sw ? bswap16(2) : 2, vmin = sw ? bswap16(4) : 4;
+	const uint32_t zero = 0, snap = sw ? bswap32(65535) : 65535;
+	const uint32_t lt = sw ? bswap32(p->linktype) : p->linktype;
+	memcpy(h, &p->magic_raw, 4);
+	memcpy(h + 4, &vmaj, 2);
+	memcpy(h + 6, &vmin, 2);
+	memcpy(h + 8, &zero, 4);
+	memcpy(h + 12, &zero, 4);
+	memcpy(h + 16, &snap, 4);
+	memcpy(h + 20, &lt, 4);
+	return write_all(fd, h, sizeof(h));
+}
+
+// As nsd_replay_pcap; with pcap_fd >= 0 also the `--out f.pcap` write-out
+// of read_pcap (netsniff-ng.c:636, 693-697, 739-746): the file header, then
+// every record that passed the filter exactly as it was read (record header
+// incl. the *_LL cooked header, then its bytes: write_pcap(fdo, &phdr, magic,
+// out, pcap_get_length) of pcap_sg.c / pcap_rw.c), in file order.
+extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_prog *filter, int out_fd,
+				    int cols, uint64_t *counters, int threads, int pcap_fd)
+{
 	if (threads <= 0) {
 		const unsigned hc = std::thread::hardware_concurrency();
 		threads = hc ? (int)(hc < 16 ? hc : 16) : 1;
@@ -251,6 +315,10 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 	const int lt = (int)p->linktype;
 	const bool has_ll = p->ll_extra != 0;   // *_LL file: one sockaddr_ll per record
 	const uint32_t ext_words = 64 * BATCH;
+	if (pcap_fd >= 0 && !push_fhdr(p, pcap_fd)) {
+		nsd_pcap_close(p);
+		return NSD_ERR_ARG;
+	}
 	nsd_pipe *pipe = nsd_pipe_create(BATCH, FRAME_BYTES, ext_words, DEPTH, lt, mode);
 	if (!pipe) {
 		nsd_pcap_close(p);
@@ -260,6 +328,7 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 		uint8_t *frames = nullptr;
 		nsd_desc_t *desc = nullptr;
 		nsd_sll_t *sll = nullptr;
+		uint8_t *rhdr = nullptr;   // record headers as read (pcap write-out)
 		nsd_rec *rec = nullptr;
 		uint32_t *ext = nullptr;
 		uint32_t *verdict = nullptr;
@@ -280,7 +349,10 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 		x.verdict = (uint32_t *)malloc(BATCH * sizeof(uint32_t));
 		if (has_ll)
 			x.sll = (nsd_sll_t *)nsd_host_alloc(BATCH * sizeof(nsd_sll_t));
-		if (!x.frames || !x.desc || !x.rec || !x.ext || !x.verdict || (has_ll && !x.sll))
+		if (pcap_fd >= 0)
+			x.rhdr = (uint8_t *)malloc((size_t)BATCH * 32);
+		if (!x.frames || !x.desc || !x.rec || !x.ext || !x.verdict || (has_ll && !x.sll) ||
+		    (pcap_fd >= 0 && !x.rhdr))
 			rc = NSD_ERR_NOMEM;
 	}
 	// complete the oldest batch and print it
@@ -347,6 +419,15 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 			w += r;
 			wn -= (size_t)r;
 		}
+		if (pcap_fd >= 0) {
+			std::string rec_out;
+			for (uint32_t k = 0; k < x.n; k++) {
+				rec_out.append((const char *)x.rhdr + 32 * (size_t)k, p->hdrsize);
+				rec_out.append((const char *)x.frames + NSD_DESC_OFF(x.desc[k]), NSD_DESC_CAPLEN(x.desc[k]));
+			}
+			if (!write_all(pcap_fd, rec_out.data(), rec_out.size()))
+				return NSD_ERR_ARG;
+		}
 		printed += x.n;
 		return NSD_OK;
 	};
@@ -355,7 +436,7 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 		Batch &x = b[slot];
 		if (x.busy && (rc = finish(x)) != NSD_OK)
 			break;
-		long n = nsd_pcap_read_batch_sll(p, x.frames, FRAME_BYTES, x.desc, x.sll, BATCH, nullptr, nullptr);
+		long n = read_batch(p, x.frames, FRAME_BYTES, x.desc, x.sll, BATCH, nullptr, nullptr, x.rhdr);
 		if (n < 0) {
 			rc = n;
 			break;
@@ -379,6 +460,8 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 				if (x.verdict[k]) {
 					if (x.sll)
 						x.sll[m] = x.sll[k];
+					if (x.rhdr && m != k)
+						memcpy(x.rhdr + 32 * (size_t)m, x.rhdr + 32 * (size_t)k, 32);
 					x.desc[m++] = x.desc[k];
 				}
 			n = m;
@@ -409,6 +492,7 @@ extern "C" long nsd_replay_pcap(const char *path, int mode, const nsd_bpf_prog *
 		nsd_host_free(x.frames);
 		nsd_host_free(x.desc);
 		nsd_host_free(x.sll);
+		free(x.rhdr);
 		nsd_host_free(x.rec);
 		nsd_host_free(x.ext);
 		free(x.verdict);

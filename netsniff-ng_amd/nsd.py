@@ -70,7 +70,8 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_pcap_open", "nsd_pcap_linktype", "nsd_pcap_read_batch", "nsd_pcap_close",
                "nsd_replay_pcap", "nsd_t3_block_desc", "nsd_dissect_device_sll",
                "dissector_entry_batch_sll", "nsd_format_packet_sll", "nsd_format_batch_sll",
-               "nsd_pipe_submit_sll", "nsd_pcap_read_batch_sll", "nsd_t3_block_desc_sll"]
+               "nsd_pipe_submit_sll", "nsd_pcap_read_batch_sll", "nsd_t3_block_desc_sll",
+               "nsd_replay_pcap_out"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -170,6 +171,8 @@ def lib():
         L.nsd_format_batch_sll.argtypes = [_vp, _vp, _vp, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]
         L.nsd_t3_block_desc.restype = ctypes.c_long
         L.nsd_t3_block_desc.argtypes = [_vp, _sz, _int, _int, _vp, _u32]
+        L.nsd_replay_pcap_out.restype = ctypes.c_long
+        L.nsd_replay_pcap_out.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp, _int, _int]
         L.nsd_t3_block_desc_sll.restype = ctypes.c_long
         L.nsd_t3_block_desc_sll.argtypes = [_vp, _sz, _int, _int, _vp, _vp, _u32]
         L.nsd_pcap_read_batch_sll.restype = ctypes.c_long
@@ -455,24 +458,32 @@ def pcap_read(path, cap=64 << 20, max_n=1 << 16, sll=False):
         L.nsd_pcap_close(h)
 
 
-def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None, threads=0, out_fd=None):
+def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None, threads=0, out_fd=None,
+                pcap_out=None):
     """`netsniff-ng --in path` through the device: returns (records printed,
     text bytes), or (records printed, None) when writing to out_fd.
-    prog: a BpfProgram (or None)."""
+    prog: a BpfProgram (or None).  pcap_out: path of the `--out f.pcap`
+    write-out (nsd_replay_pcap_out), or None."""
     import tempfile
     L = lib()
     cnt = counters if counters is not None else np.zeros(NCOUNTERS, dtype=np.uint64)
     h = prog.h if prog is not None else None
-    if out_fd is not None:
-        n = L.nsd_replay_pcap(os.fsencode(path), mode, h, out_fd, cols, cnt.ctypes.data, threads)
-        _check(0 if n >= 0 else n, "nsd_replay_pcap")
-        return n, None
-    with tempfile.TemporaryFile() as f:
-        n = L.nsd_replay_pcap(os.fsencode(path), mode, h, f.fileno(), cols, cnt.ctypes.data, threads)
-        if n < 0:
-            raise NsdError(f"nsd_replay_pcap failed with status {n}")
-        f.seek(0)
-        return n, f.read()
+    pfd = os.open(pcap_out, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o644) if pcap_out else -1
+    try:
+        if out_fd is not None:
+            n = L.nsd_replay_pcap_out(os.fsencode(path), mode, h, out_fd, cols, cnt.ctypes.data, threads, pfd)
+            _check(0 if n >= 0 else n, "nsd_replay_pcap_out")
+            return n, None
+        with tempfile.TemporaryFile() as f:
+            n = L.nsd_replay_pcap_out(os.fsencode(path), mode, h, f.fileno(), cols, cnt.ctypes.data, threads,
+                                      pfd)
+            if n < 0:
+                raise NsdError(f"nsd_replay_pcap_out failed with status {n}")
+            f.seek(0)
+            return n, f.read()
+    finally:
+        if pfd >= 0:
+            os.close(pfd)
 
 
 def t3_block_desc(block, packet_type=-1, lo_ifindex=-1, max_n=1 << 16, sll=False):
