@@ -4,16 +4,35 @@ Workload (BASELINE.json configs[1], "C2"): 16,777,216 synthetic 64 B
 Eth/IPv4/UDP frames per GPU, resident in HBM; one step = one pass of the
 dissector chain kernel over the batch (records + ext + per-protocol counters)
 plus, for N > 1 GPUs, the RCCL all-reduce of the counter vector.
---config imix / ipv6x select C3 / C4 instead.
+--config imix / ipv6x select C3 / C4 as the headline instead; --shards S
+walks S contiguous 16M shards of the same stream as one batch on one GPU
+(--config imix --shards 8 = C5's 128M packets on a single MI355X).
+
+The same run also measures, beside the headline (rank 0, N = 1):
+  legs        C3 (IMIX; the metric is "64B & IMIX") and C4 as their own
+              measured objects (kernel time, roofline, traffic);
+  traffic     HBM bytes per launch from rocprofv3 PMC counters, collected
+              in-run by two child processes (FETCH_SIZE and WRITE_SIZE in
+              separate passes, MI355X_MICROARCH.md "HBM") before this
+              process touches the GPU;
+  cpu_baseline the CPU restatement (oracle, "port") on this host's cores:
+              fields + text (what the reference does: it prints as it
+              parses) and fields only, 1 thread and all threads;
+  end_to_end / replay / bpf_filter (reported, never `value`).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, weak scaling: every rank walks its
 own 16M-packet shard).  Rank 0 prints one JSON line.
 """
 import argparse
+import csv
+import glob
+import hashlib
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -31,40 +50,206 @@ CONFIGS = {
     "imix": dict(cfg=T.SYN_IMIX, name="C3: 16M IMIX 64/576/1500 Eth/[VLAN]/IPv4/{TCP,UDP,ICMP}"),
     "ipv6x": dict(cfg=T.SYN_IPV6X, name="C4: 16M IPv6 + 0..6 extension headers"),
 }
+LEGS = ("imix", "ipv6x")
 HBM_PEAK_GBS = 8000.0      # MI355X spec (MI355X_MICROARCH.md)
 REC_B, DESC_B = 16, 8
+MODES = ["PRINT_NORM", "PRINT_LESS", "PRINT_HEX", "PRINT_ASCII", "PRINT_HEX_ASCII", "PRINT_NONE"]
 
 
-def wsum_for(cfg_key, n, lo):
-    """Sum of algorithmic read bytes W over the shard (DESIGN.md "Roofline").
-    C2: every frame is 64 B, W = caplen.  C3/C4: committed per-config sums
-    (tests/golden/wsum.json, made by tests/golden/make_golden.py from the CPU
-    restatement) for the standard 16M shard at lo = 0, else None."""
-    if cfg_key == "udp64":
-        return 64 * n
+def workload_name(key, n, shards):
+    if shards > 1:
+        return (f"C5 on one GPU: {shards} x {n // (1 << 20)}M-packet IMIX shards ({shards * n} packets)"
+                if key == "imix" else f"{CONFIGS[key]['name']} x {shards} shards")
+    return CONFIGS[key]["name"]
+
+
+def wsum_for(key, n, lo, shards=1):
+    """Sum of algorithmic read bytes W over [lo, lo + shards*n) (DESIGN.md
+    "Roofline").  C2: every frame is 64 B, W = caplen.  C3/C4: committed
+    per-shard sums (tests/golden/wsum.json, made by make_golden.py from the
+    CPU restatement; shard keys lo:n), else None."""
+    if key == "udp64":
+        return 64 * n * shards
     path = os.path.join(ROOT, "tests", "golden", "wsum.json")
-    if os.path.exists(path):
-        with open(path) as f:
-            table = json.load(f)
-        key = f"{cfg_key}:{lo}:{n}"
-        if key in table:
-            return int(table[key])
-    return None
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        table = json.load(f)
+    total = 0
+    for r in range(shards):
+        k = f"{key}:{lo + r * n}:{n}"
+        if k not in table:
+            return None
+        total += int(table[k])
+    return total
 
 
-def cpu_baseline(cfg, n_sample, threads, seconds):
-    """CPU restatement (oracle, "port") timed on this host: the fields-only
-    walk (records + counters, no text) with `threads` threads, repeated over
-    one resident sample of `n_sample` packets until `seconds` have passed.
-    Returns (Mpkt/s, packets walked, seconds)."""
+def library_info():
+    L = nsd.lib()
+    with open(nsd.LIB_PATH, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    return {"path": os.path.relpath(nsd.LIB_PATH, ROOT), "sha256_16": sha,
+            "version": L.nsd_version().decode(), "build": L.nsd_build_info().decode()}
+
+
+# ---- device batches --------------------------------------------------------------
+class Batch:
+    """A config's packets resident in HBM plus the output buffers of one walk."""
+
+    def __init__(self, key, n, lo, shards, dev):
+        self.key, self.n_shard, self.shards = key, n, shards
+        self.n = n * shards
+        cfg = CONFIGS[key]["cfg"]
+        self.frames, self.desc, desc_np = T.make_device_batch(cfg, self.n, lo=lo, device=dev)
+        caps = T.desc_caplen(desc_np)
+        self.frame_bytes = int(caps.sum())
+        self.line_bytes = int(np.minimum(caps, 64).sum())   # first 64-B line per frame (BPF leg)
+        del desc_np
+        ext_w = nsd.ext_pool_words(self.n) if key == "ipv6x" else nsd.ext_pool_words(self.n // 64)
+        self.rec = torch.empty(self.n * REC_B, dtype=torch.uint8, device=dev)
+        self.ext = torch.empty(ext_w, dtype=torch.int32, device=dev)
+        self.ext_used = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.counters = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device=dev)
+        self.ws = torch.empty(nsd.lib().nsd_workspace_bytes(self.n), dtype=torch.uint8, device=dev)
+        self.wsum = wsum_for(key, n, lo, shards)
+
+    def step(self, mode, grid=0, ev=None):
+        self.ext_used.zero_()
+        self.counters.zero_()
+        if ev is not None:
+            ev[0].record()
+        nsd.dissect_device(self.frames, self.desc, mode=mode, rec=self.rec, ext=self.ext,
+                           ext_used=self.ext_used, counters=self.counters, grid=grid, workspace=self.ws)
+        if ev is not None:
+            ev[1].record()
+
+    def roofline(self, kern_ms, traffic=None, copy_gbs=None):
+        if self.wsum is None:
+            return None
+        read_b = DESC_B * self.n + self.wsum
+        total_b = read_b + REC_B * self.n
+        achieved = total_b / (kern_ms * 1e-3) / 1e9
+        r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(achieved / HBM_PEAK_GBS, 4),
+             "traffic": None if traffic is None else round(traffic["bytes_per_launch"]),
+             "read_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+             "bytes_per_pkt": {"read": round(read_b / self.n, 2), "write": REC_B},
+             "kernel_ms": round(kern_ms, 4)}
+        if traffic is not None:
+            r["traffic_bytes_per_pkt"] = {"read": round(traffic["read_bytes"] / self.n, 1),
+                                          "write": round(traffic["write_bytes"] / self.n, 1)}
+        if copy_gbs:
+            r["copy_gbs"] = round(copy_gbs, 1)
+            r["frac_of_copy"] = round(achieved / copy_gbs, 4)
+        return r
+
+    def free(self):
+        for a in ("frames", "desc", "rec", "ext", "ext_used", "counters", "ws"):
+            setattr(self, a, None)
+
+
+def time_steps(b, mode, steps, warmup, grid=0):
+    """Kernel time per launch (HIP events on the launch stream = torch's current one)."""
+    for _ in range(warmup):
+        b.step(mode, grid)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for k in range(steps):
+        b.step(mode, grid, evs[k])
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(c) for a, c in evs]))
+
+
+# ---- in-run PMC traffic ----------------------------------------------------------
+def pmc_child(args):
+    """Runs under rocprofv3 --pmc: `steps` dissect launches per config, in
+    the order of --pmc-configs (the parent splits the dispatches by order)."""
+    torch.cuda.set_device(0)
+    for key in args.pmc_configs.split(","):
+        shards = args.shards if key == args.config else 1
+        b = Batch(key, args.packets, 0, shards, torch.device("cuda", 0))
+        for _ in range(args.steps):
+            b.step(args.mode, args.grid)
+        torch.cuda.synchronize()
+        b.free()
+        torch.cuda.empty_cache()
+
+
+def pmc_traffic(args, keys, steps=3):
+    """HBM bytes per dissect launch for each config in `keys`, from two
+    rocprofv3 --pmc child runs (FETCH_SIZE, WRITE_SIZE: separate passes).
+    FETCH_SIZE counts half the bytes of a wide coalesced read on gfx950 and is
+    doubled; both are KiB (MI355X_MICROARCH.md "HBM").  Returns
+    {key: {...}} or {"error": ...}."""
+    got = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory(dir="/tmp") as d:
+            cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", ctr, "--kernel-trace", "-d", d, "-o",
+                   "run", "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__),
+                   "--pmc-child", "--pmc-configs", ",".join(keys), "--config", args.config,
+                   "--packets", str(args.packets), "--shards", str(args.shards), "--steps", str(steps),
+                   "--mode", str(args.mode), "--grid", str(args.grid)]
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                return {"error": f"rocprofv3 --pmc {ctr} rc={r.returncode}: "
+                                 + r.stdout.decode(errors="replace")[-300:]}
+            rows = []
+            for fn in files:
+                with open(fn) as f:
+                    for j, row in enumerate(csv.DictReader(f)):
+                        if "dissect_all" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                            order = row.get("Dispatch_Id") or row.get("Correlation_Id") or j
+                            rows.append((int(order), float(row["Counter_Value"])))
+            rows.sort()
+            if len(rows) != steps * len(keys):
+                return {"error": f"{ctr}: {len(rows)} dissect dispatches, expected {steps * len(keys)}"}
+            for i, key in enumerate(keys):
+                v = [x for _, x in rows[i * steps:(i + 1) * steps]]
+                got.setdefault(key, {})[ctr] = sum(v) / len(v) * 1024
+    out = {}
+    for key in keys:
+        rd, wr = 2 * got[key]["FETCH_SIZE"], got[key]["WRITE_SIZE"]
+        out[key] = {"read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr}
+    return out
+
+
+# ---- CPU baseline ------------------------------------------------------------------
+def cpu_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, avail
+
+
+def cpu_rate(cfg, n_sample, threads, seconds, text):
+    """CPU restatement (oracle, "port") over one resident sample of
+    `n_sample` packets, repeated until `seconds` have passed: fields only
+    (records + counters) or fields + PRINT_NORM text (per-packet sink,
+    discarded like a write to /dev/null).  Returns (Mpkt/s, packets, s)."""
     frames, desc = T.make_batch(cfg, n_sample, lo=0, threads=threads)
     lib = T.oracle()
     counters = np.zeros(64, dtype=np.uint64)
     rec = np.zeros(n_sample, dtype=T.REC_DTYPE)
+    tb = np.zeros(1, dtype=np.uint64)
     done, t0 = 0, time.perf_counter()
     while True:
-        lib.nsor_dissect_batch_mt(frames.ctypes.data, desc.ctypes.data, n_sample, 1, T.PRINT_NORM,
-                                  rec.ctypes.data, counters.ctypes.data, threads)
+        if text:
+            lib.nsor_dissect_batch_text_mt(frames.ctypes.data, desc.ctypes.data, n_sample, 1, T.PRINT_NORM,
+                                           threads, tb.ctypes.data)
+        else:
+            lib.nsor_dissect_batch_mt(frames.ctypes.data, desc.ctypes.data, n_sample, 1, T.PRINT_NORM,
+                                      rec.ctypes.data, counters.ctypes.data, threads)
         done += n_sample
         dt = time.perf_counter() - t0
         if dt >= seconds:
@@ -72,18 +257,37 @@ def cpu_baseline(cfg, n_sample, threads, seconds):
     return done / dt / 1e6, done, dt
 
 
-def bpf_bench(frames, desc, n, line_bytes, steps, warmup):
+def cpu_baseline(key, seconds):
+    cfg = CONFIGS[key]["cfg"]
+    model, nproc, avail = cpu_info()
+    threads = min(avail, 16)   # the GPU box's CPU share per GPU is 16 threads
+    t1, p1, d1 = cpu_rate(cfg, 1 << 16, 1, seconds / 4, True)
+    tN, pN, dN = cpu_rate(cfg, 1 << 20, threads, seconds / 4, True)
+    f1, q1, e1 = cpu_rate(cfg, 1 << 20, 1, seconds / 4, False)
+    fN, qN, eN = cpu_rate(cfg, 1 << 22, threads, seconds / 4, False)
+    return {"value": round(tN, 3), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+            "sample": f"{key}: fields + PRINT_NORM text (the reference prints as it parses) by the CPU "
+                      f"restatement (oracle/nsd_oracle.c), {threads} threads over contiguous shards, "
+                      f"{pN} packets (passes over a resident 1M-packet sample) in {dN:.1f} s",
+            "cpu_model": model, "nproc": nproc, "cpus_available": avail,
+            "text_1thread": round(t1, 3),
+            "fields_only": {"threads": round(fN, 3), "1thread": round(f1, 3)},
+            "reference_harness_container": "0.182 Mpkt/s PRINT_NORM 1 core (BASELINE.md, measured in the "
+                                           "build container, not on this host)"}
+
+
+# ---- host-memory legs (reported, never `value`) ----------------------------------------
+def bpf_bench(b, steps, warmup):
     """Device BPF filter (nsd_bpf.hip) over the same resident batch:
     bpfc.8's "Only allow IPv4 TCP packets" program (ldh [12]; jne #0x800;
     ldb [23]; jneq #6; ret #-1; ret #0), verdicts only and with the compaction
     of accepted descriptors.  Algorithmic bytes per packet: 8 (descriptor) +
     the frame's first 64-B line (capped at caplen; the program reads bytes
-    12..23) + 4 (verdict); compaction adds 12 B read + 8 B per accepted packet.
-    Kernel time by HIP events on torch's current stream (the launch stream)."""
+    12..23) + 4 (verdict)."""
     prog = np.array([(0x28, 0, 0, 12), (0x15, 0, 3, 0x800), (0x30, 0, 0, 23), (0x15, 0, 1, 6),
                      (0x06, 0, 0, 0xFFFFFFFF), (0x06, 0, 0, 0)], dtype=nsd.BPF_INSN)
     bp = nsd.BpfProgram(prog)
-    dev = desc.device
+    n, dev = b.n, b.desc.device
     verdict = torch.empty(n, dtype=torch.int32, device=dev)
     out = torch.empty(n, dtype=torch.int64, device=dev)
     count = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -91,16 +295,16 @@ def bpf_bench(frames, desc, n, line_bytes, steps, warmup):
     res = {}
     for compact in (False, True):
         for _ in range(max(warmup, 1)):
-            bp.filter_device(frames, desc, compact, verdict, out, count, ws)
+            bp.filter_device(b.frames, b.desc, compact, verdict, out, count, ws)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         for _ in range(steps):
-            bp.filter_device(frames, desc, compact, verdict, out, count, ws)
+            bp.filter_device(b.frames, b.desc, compact, verdict, out, count, ws)
         ev[1].record()
         torch.cuda.synchronize()
         res[compact] = ev[0].elapsed_time(ev[1]) / steps
     kept = int(count.item())
-    algo = 8 * n + line_bytes + 4 * n
+    algo = 8 * n + b.line_bytes + 4 * n
     gbs = algo / (res[False] * 1e-3) / 1e9
     bp.close()
     return {"program": "bpfc.8 'Only allow IPv4 TCP packets' (6 insns)", "accepted": kept,
@@ -115,7 +319,7 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
     """Host memory in, records in host memory out: `nbatch`
     batches of `batch` packets from one pinned host buffer go through the
     pipelined path (nsd_pipe_*: H2D, dissect kernels, D2H of records, ext and
-    counters, `depth` batches in flight).  Returns a dict for the JSON line."""
+    counters, `depth` batches in flight)."""
     L = nsd.lib()
     n = batch * nbatch
     frames, desc = T.make_batch(cfg, n, lo=0, threads=16)
@@ -168,9 +372,7 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
 def replay_leg(cfg, n, mode, threads, reps=2):
     """`netsniff-ng --in file.pcap` through the device (nsd_replay_pcap): a
     synthetic pcap of n records in a temp file -> reader -> pipelined device
-    walk -> host formatter on `threads` threads -> /dev/null.  Reported
-    beside the device-resident number; never `value`."""
-    import tempfile
+    walk -> host formatter on `threads` threads -> /dev/null."""
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "replay.pcap")
         T.synth().nsd_synth_pcap(cfg, T.SEED, 0, n, path.encode())
@@ -192,91 +394,9 @@ def replay_leg(cfg, n, mode, threads, reps=2):
                     "formatter -> /dev/null (nsd_replay_pcap), best of %d" % reps}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="udp64", choices=sorted(CONFIGS))
-    ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
-    ap.add_argument("--mode", type=int, default=nsd.PRINT_NORM)
-    ap.add_argument("--grid", type=int, default=0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="packets in the CPU sample")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline duration")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end pass")
-    ap.add_argument("--no-bpf", action="store_true", help="skip the device BPF filter pass")
-    ap.add_argument("--no-replay", action="store_true", help="skip the pcap replay (--in) pass")
-    ap.add_argument("--replay-packets", type=int, default=1 << 20)
-    ap.add_argument("--e2e-batch", type=int, default=1 << 20)
-    ap.add_argument("--e2e-batches", type=int, default=16)
-    ap.add_argument("--e2e-depth", type=int, default=3)
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        dist = None
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
-
-    c = CONFIGS[args.config]
-    n = args.packets
-    lo = rank * n
-    frames_np, desc_np = T.make_batch(c["cfg"], n, lo=lo, threads=16)
-    frames = torch.from_numpy(frames_np).to(dev)
-    desc = torch.from_numpy(desc_np.view(np.int64)).to(dev)
-    frame_bytes = int(T.desc_caplen(desc_np).sum())
-    line_bytes = int(np.minimum(T.desc_caplen(desc_np), 64).sum())   # first 64-B line per frame
-    del frames_np
-    ext_w = nsd.ext_pool_words(n) if args.config == "ipv6x" else nsd.ext_pool_words(n // 64)
-    rec = torch.empty(n * REC_B, dtype=torch.uint8, device=dev)
-    ext = torch.empty(ext_w, dtype=torch.int32, device=dev)
-    ext_count = torch.zeros(1, dtype=torch.int32, device=dev)
-    counters = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device=dev)
-    workspace = torch.empty(nsd.lib().nsd_workspace_bytes(n), dtype=torch.uint8, device=dev)
-
-    def step(ev=None):
-        ext_count.zero_()
-        counters.zero_()
-        if ev is not None:
-            ev[0].record()
-        nsd.dissect_device(frames, desc, mode=args.mode, rec=rec, ext=ext, ext_used=ext_count,
-                           counters=counters, grid=args.grid, workspace=workspace)
-        if ev is not None:
-            ev[1].record()
-        if dist is not None:
-            dist.all_reduce(counters)   # RCCL over xGMI: per-protocol counters
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
-    # achievable streaming rate on this device: a 1 GiB
-    # device-to-device copy, read + write bytes / time
+def copy_rate(dev):
+    """Achievable streaming rate on this device: a 1 GiB
+    device-to-device copy, read + write bytes / time."""
     cbuf = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
     cdst = torch.empty_like(cbuf)
     for _ in range(2):
@@ -287,56 +407,128 @@ def main():
         cdst.copy_(cbuf)
     ce[1].record()
     torch.cuda.synchronize()
-    copy_gbs = 2 * cbuf.numel() * 5 / (ce[0].elapsed_time(ce[1]) * 1e-3) / 1e9
+    gbs = 2 * cbuf.numel() * 5 / (ce[0].elapsed_time(ce[1]) * 1e-3) / 1e9
     del cbuf, cdst
+    return gbs
 
-    bpf = None if args.no_bpf else bpf_bench(frames, desc, n, line_bytes, args.steps, args.warmup)
 
-    cnt = counters.cpu().numpy().view(np.uint64)
-    total_pkts = n * world
-    # (experiment builds that skip a phase on purpose set NSD_BENCH_NOCHECK)
-    assert int(cnt[nsd.CNT_PKTS]) == total_pkts or os.environ.get("NSD_BENCH_NOCHECK"), \
-        "counter check failed"
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="udp64", choices=sorted(CONFIGS))
+    ap.add_argument("--packets", type=int, default=1 << 24, help="packets per shard")
+    ap.add_argument("--shards", type=int, default=1, help="contiguous shards walked as one batch per GPU")
+    ap.add_argument("--mode", type=int, default=nsd.PRINT_NORM)
+    ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="CPU baseline duration (4 legs)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end pass")
+    ap.add_argument("--no-bpf", action="store_true", help="skip the device BPF filter pass")
+    ap.add_argument("--no-replay", action="store_true", help="skip the pcap replay (--in) pass")
+    ap.add_argument("--no-legs", action="store_true", help="skip the C3 / C4 legs")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the in-run rocprofv3 PMC traffic pass")
+    ap.add_argument("--replay-packets", type=int, default=1 << 20)
+    ap.add_argument("--e2e-batch", type=int, default=1 << 20)
+    ap.add_argument("--e2e-batches", type=int, default=16)
+    ap.add_argument("--e2e-depth", type=int, default=3)
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-configs", default="", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.pmc_child:
+        pmc_child(args)
+        return
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    solo = rank == 0 and world == 1
+    legs = [k for k in LEGS if k != args.config] if solo and not args.no_legs else []
+
+    # PMC traffic first, in child processes, before this process initialises the GPU
+    traffic = None
+    if solo and not args.no_pmc:
+        traffic = pmc_traffic(args, [args.config] + legs)
+
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    n = args.packets
+    lo = rank * n * args.shards
+    b = Batch(args.config, n, lo, args.shards, dev)
+
+    for _ in range(args.warmup):
+        b.step(args.mode, args.grid)
+        if dist is not None:
+            dist.all_reduce(b.counters)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        b.step(args.mode, args.grid, evs[k])
+        if dist is not None:
+            dist.all_reduce(b.counters)   # RCCL over xGMI: per-protocol counters
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(c) for a, c in evs]))
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    cnt = b.counters.cpu().numpy().view(np.uint64)
+    total_pkts = b.n * world
+    assert int(cnt[nsd.CNT_PKTS]) == total_pkts, "counter check failed"
     ms_per_step = elapsed / args.steps * 1e3
     mpps = total_pkts * args.steps / elapsed / 1e6
 
-    wsum = wsum_for(args.config, n, lo)
-    roofline = None
-    if wsum is not None:
-        read_b = DESC_B * n + wsum
-        total_b = read_b + REC_B * n
-        achieved = total_b / (kern_ms * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": None,
-                    "read_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "bytes_per_pkt": {"read": round(read_b / n, 2), "write": REC_B},
-                    "kernel_ms": round(kern_ms, 4),
-                    "copy_gbs": round(copy_gbs, 1),
-                    "frac_of_copy": round(achieved / copy_gbs, 4)}
-        prof = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-        if os.path.exists(prof):
-            with open(prof) as f:
-                roofline["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+    copy_gbs = copy_rate(dev)
+    tr = traffic.get(args.config) if isinstance(traffic, dict) else None
+    roofline = b.roofline(kern_ms, tr, copy_gbs)
+    bpf = None if args.no_bpf or not solo else bpf_bench(b, args.steps, args.warmup)
+    frame_bytes = b.frame_bytes
+    b.free()
+    torch.cuda.empty_cache()
+
+    leg_out = {}
+    for key in legs:
+        lb = Batch(key, n, 0, 1, dev)
+        ms = time_steps(lb, args.mode, args.steps, args.warmup, args.grid)
+        lc = lb.counters.cpu().numpy().view(np.uint64)
+        assert int(lc[nsd.CNT_PKTS]) == lb.n, f"{key}: counter check failed"
+        ltr = traffic.get(key) if isinstance(traffic, dict) else None
+        leg_out[key] = {"workload": CONFIGS[key]["name"], "packets": lb.n,
+                        "value": round(lb.n / (ms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
+                        "gbps_frames": round(lb.frame_bytes / (ms * 1e-3) / 1e9, 1),
+                        "roofline": lb.roofline(ms, ltr, copy_gbs)}
+        lb.free()
+        torch.cuda.empty_cache()
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        threads = min(os.cpu_count() or 1, 16)
-        v1, p1, d1 = cpu_baseline(c["cfg"], args.cpu_sample // 4, 1, args.cpu_seconds / 2)
-        vN, pN, dN = cpu_baseline(c["cfg"], args.cpu_sample, threads, args.cpu_seconds)
-        cpu = {"value": round(vN, 3), "unit": "Mpkt/s", "cores": threads, "kind": "port",
-               "sample": f"{args.config}: {pN} packets ({pN // args.cpu_sample} passes over a resident"
-                         f" {args.cpu_sample}-packet sample) in {dN:.1f} s, fields-only restatement"
-                         f" walk (oracle/nsd_oracle.c), {threads} threads; 1 thread:"
-                         f" {v1:.3f} Mpkt/s ({p1} packets, {d1:.1f} s)"}
+    if solo and not args.no_cpu:
+        cpu = cpu_baseline(args.config, args.cpu_seconds)
 
     e2e = None
-    if rank == 0 and world == 1 and not args.no_e2e:
-        e2e = end_to_end(c["cfg"], args.e2e_batch, args.e2e_batches, args.e2e_depth, args.mode)
+    if solo and not args.no_e2e:
+        e2e = end_to_end(CONFIGS[args.config]["cfg"], args.e2e_batch, args.e2e_batches, args.e2e_depth, args.mode)
 
     replay = None
-    if rank == 0 and world == 1 and not args.no_replay:
-        replay = replay_leg(c["cfg"], args.replay_packets, args.mode, min(os.cpu_count() or 1, 16))
+    if solo and not args.no_replay:
+        replay = replay_leg(CONFIGS[args.config]["cfg"], args.replay_packets, args.mode, min(cpu_info()[2], 16))
 
     if rank == 0:
         out = {
@@ -345,17 +537,20 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (seeded splitmix64 generators, tools/nsd_synth.c)",
-            "config": {"workload": c["name"], "packets_per_gpu": n, "frame_bytes_per_gpu": frame_bytes,
-                       "mode": ["PRINT_NORM", "PRINT_LESS", "PRINT_HEX", "PRINT_ASCII",
-                                "PRINT_HEX_ASCII", "PRINT_NONE"][args.mode],
+            "config": {"workload": workload_name(args.config, n, args.shards), "packets_per_gpu": b.n,
+                       "frame_bytes_per_gpu": frame_bytes, "mode": MODES[args.mode],
                        "parallelism": f"dp{world}"},
             "gbps_frames": round(frame_bytes * world * args.steps / elapsed / 1e9, 1),
             "roofline": roofline,
+            "legs": leg_out or None,
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "replay": replay,
             "bpf_filter": bpf,
+            "library": library_info(),
         }
+        if isinstance(traffic, dict) and "error" in traffic:
+            out["pmc_error"] = traffic["error"]
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

@@ -417,6 +417,8 @@ int nsd_host_unregister(void *ptr);
 
 /* Library / device info. */
 const char *nsd_version(void);
+/* the compile line the library was built with (bench lines record it) */
+const char *nsd_build_info(void);
 int nsd_device_count(void);
 
 #ifdef __cplusplus

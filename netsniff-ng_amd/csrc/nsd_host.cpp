@@ -437,7 +437,12 @@ extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype,
 	emit(s);
 }
 
-extern "C" const char *nsd_version(void) { return "netsniff-dissect 0.1 (gfx950)"; }
+extern "C" const char *nsd_version(void) { return "netsniff-dissect 0.2 (gfx950)"; }
+
+#ifndef NSD_BUILD_INFO
+#define NSD_BUILD_INFO "unknown"
+#endif
+extern "C" const char *nsd_build_info(void) { return NSD_BUILD_INFO; }
 
 extern "C" int nsd_device_count(void)
 {

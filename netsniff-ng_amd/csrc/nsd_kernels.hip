@@ -304,12 +304,8 @@ __device__ __forceinline__ uint16_t csum_final(uint32_t sum)
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store_rec(uint4 *rec, uint32_t i, uint4 r)
 {
-#ifdef NSD_X_PLAINREC
-	rec[i] = r;
-#else
 	const v4u v = { r.x, r.y, r.z, r.w };
 	__builtin_nontemporal_store(v, (v4u *)(rec + i));
-#endif
 }
 
 // record words of a finished walk (layout of nsd_rec)
@@ -483,11 +479,7 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 		if (valid) {
 			const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
 					      (uint32_t)off & 15, 0, false };
-#ifdef NSD_X_NOWALK
-			w.chain = src.dw(3) & 0x3FF; w.n = 2; w.data = 42;
-#else
 			fw = fast_walk<MODE>(src, caplen, w);
-#endif
 		}
 		const bool deferred = fw != FW_DONE;
 		wave_sync_lds();
@@ -719,7 +711,6 @@ __device__ __forceinline__ uint32_t pass2(Shared &sh, const uint8_t *__restrict_
 			}
 			if (ex && w.slot == 0xFFFFFFFFu)
 				w.flags |= NSD_F_OVERFLOW;   // the pool is full
-#ifndef NSD_X_NOEXTW
 			if (ex && w.slot != 0xFFFFFFFFu) {
 				uint32_t *e = ext + w.slot;
 				const uint32_t nl = w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS;
@@ -737,7 +728,6 @@ __device__ __forceinline__ uint32_t pass2(Shared &sh, const uint8_t *__restrict_
 				if (nl > 12)
 					*(uint4 *)(e + 16) = make_uint4(lv(12), lv(13), lv(14), lv(15));
 			}
-#endif
 		}
 		if (fin)
 			store_rec(rec, i, pack_record(w));
@@ -865,13 +855,11 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 		pass1<MODE>(sh, frames, desc, n, start_id, rec, queue, region, pend, (uint32_t)c0, end, npend);
 		if (MODE == PRINT_NORM || MODE == PRINT_LESS) {
 			__syncthreads();   // the span's queue entries and sh.qn are complete
-#ifndef NSD_X_NOP2
 			// (waves take queue entries dynamically and pass 2 has no block
 			// barrier, so fewer walkers only changes who drains the queue)
 			if ((threadIdx.x >> 6) < NSD_P2_WAVES)
 				q0 = pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, ext,
 						 ext_words, ext_used, chunk, q0, sll);
-#endif
 			__syncthreads();   // every wave is done taking entries: restart the taker at q0
 			if (threadIdx.x == 0)
 				sh.q2 = q0;
@@ -881,9 +869,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 		sh.pcnt[threadIdx.x >> 6] = npend;
 	if (MODE == PRINT_NORM) {
 		__syncthreads();   // records final, pending lists and counts complete
-#ifndef NSD_X_NOICMP
 		icmp_pass<NSD_CSUM_U>(sh, frames, desc, rec, pend, pend2, region);
-#endif
 	}
 	block_flush(sh.cnt, counters);
 }

@@ -266,9 +266,7 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 	w.offB |= act && k >= 4 && k < NSD_REC_MAX_LAYERS ? (start & 0xFFFF) << (16 * (kk & 1)) : 0u;
 	w.flags |= act && k >= NSD_EXT_MAX_LAYERS ? NSD_F_OVERFLOW : 0;
 	if (act && k < NSD_EXT_MAX_LAYERS) {
-#ifndef NSD_X_NOCNT
 		atomicAdd(&g.s_cnt[NSD_CNT_OPS + id], 1ull);   // the oracle counts the first 64 layers
-#endif
 		const uint32_t lv = (uint32_t)id | start << 16;
 		if (k >= NSD_REC_MAX_LAYERS && k < DEEP)
 			g.lay[(k - NSD_REC_MAX_LAYERS) * 64 + __lane_id()] = lv;

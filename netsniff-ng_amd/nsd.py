@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("NSD_LIB") or os.path.join(HERE, "libnsdissect.so")
+LIB_PATH = os.path.join(HERE, "libnsdissect.so")
 
 PRINT_NORM, PRINT_LESS, PRINT_HEX, PRINT_ASCII, PRINT_HEX_ASCII, PRINT_NONE = range(6)
 LINKTYPE_EN10MB = 1
@@ -71,7 +71,7 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_replay_pcap", "nsd_t3_block_desc", "nsd_dissect_device_sll",
                "dissector_entry_batch_sll", "nsd_format_packet_sll", "nsd_format_batch_sll",
                "nsd_pipe_submit_sll", "nsd_pcap_read_batch_sll", "nsd_t3_block_desc_sll",
-               "nsd_replay_pcap_out"]
+               "nsd_replay_pcap_out", "nsd_build_info"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -119,6 +119,7 @@ def lib():
         L.nsd_tprintf_wrap.argtypes = [ctypes.c_char_p, _sz, _int, ctypes.POINTER(ctypes.c_long),
                                        ctypes.c_char_p, _sz]
         L.nsd_version.restype = ctypes.c_char_p
+        L.nsd_build_info.restype = ctypes.c_char_p
         L.nsd_device_count.restype = _int
         L.nsd_pipe_create.restype = _vp
         L.nsd_pipe_create.argtypes = [_u32, _sz, _u32, _int, _int, _int]

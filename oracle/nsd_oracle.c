@@ -1675,7 +1675,59 @@ typedef struct {
 	nsd_rec *rec;
 	uint64_t counters[NSD_NCOUNTERS];
 	uint64_t sw;
+	uint64_t text_bytes;
 } mt_job;
+
+/* fields + text (what the reference always does: it prints as it parses)
+ * per packet into a thread-local sink that is reset after every packet, as
+ * tprintf_flush empties the reference's buffer (tprintf.c:105-110) */
+static void *mt_text_worker(void *arg)
+{
+	mt_job *j = arg;
+	nsor_info in;
+	nsor_text t;
+	nsor_text_init(&t);
+	for (uint32_t i = j->lo; i < j->hi; i++) {
+		uint64_t d = j->desc[i];
+		nsor_dissect(j->frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), j->linktype, j->mode, &t,
+			     NULL, &in);
+		j->text_bytes += t.len;
+		j->sw += in.w_bytes;
+		nsor_text_reset(&t);
+	}
+	nsor_text_free(&t);
+	return NULL;
+}
+
+uint64_t nsor_dissect_batch_text_mt(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
+				    int linktype, int mode, int nthreads, uint64_t *text_bytes)
+{
+	pthread_t th[256];
+	mt_job *jobs;
+	uint64_t sw = 0, tb = 0;
+
+	if (nthreads < 1) nthreads = 1;
+	if (nthreads > 256) nthreads = 256;
+	jobs = calloc(nthreads, sizeof(*jobs));
+	for (int t = 0; t < nthreads; t++) {
+		jobs[t].frames = frames;
+		jobs[t].desc = desc;
+		jobs[t].lo = (uint32_t)((uint64_t)n * t / nthreads);
+		jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+		jobs[t].linktype = linktype;
+		jobs[t].mode = mode;
+		pthread_create(&th[t], NULL, mt_text_worker, &jobs[t]);
+	}
+	for (int t = 0; t < nthreads; t++) {
+		pthread_join(th[t], NULL);
+		sw += jobs[t].sw;
+		tb += jobs[t].text_bytes;
+	}
+	free(jobs);
+	if (text_bytes)
+		*text_bytes = tb;
+	return sw;
+}
 
 static void *mt_worker(void *arg)
 {

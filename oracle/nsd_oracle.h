@@ -77,6 +77,12 @@ uint64_t nsor_dissect_batch_mt(const uint8_t *frames, const nsd_desc_t *desc, ui
 			       int linktype, int mode, nsd_rec *rec, uint64_t *counters,
 			       int nthreads);
 
+/* Multi-threaded fields + text walk (text per packet into a per-thread sink,
+ * discarded after each packet: the formatted CPU baseline); *text_bytes
+ * receives the text length.  Returns sum W. */
+uint64_t nsor_dissect_batch_text_mt(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
+				    int linktype, int mode, int nthreads, uint64_t *text_bytes);
+
 /* Name tables (lookup.c:33-95 restated).  dir NULL => clear (names off). */
 int  nsor_lookup_init(const char *dir);
 void nsor_lookup_clear(void);

@@ -70,6 +70,38 @@ def make_batch(cfg, n, lo=0, seed=SEED, align=16, threads=8, pad=64):
     return frames, desc
 
 
+def make_device_batch(cfg, n, lo=0, seed=SEED, device="cuda", chunk=1 << 24, threads=16, on_chunk=None,
+                      pad=64):
+    """Packets [lo, lo+n) of a config generated chunk by chunk on the host
+    and copied into one device buffer (the host never holds more than one
+    chunk of frames: C5's 128M IMIX frames are 47.6 GB).  Frames are packed
+    at 16-byte boundaries from byte 0 exactly as make_batch() packs them.
+    on_chunk(a, frames_chunk, desc_chunk_rebased) is called per chunk with
+    the host copy (descriptors rebased to the chunk's first byte), e.g. for
+    oracle checks.  Returns (frames u8 cuda tensor, desc i64 cuda tensor,
+    desc numpy u64)."""
+    import torch
+    s = synth()
+    desc = np.zeros(n, dtype=np.uint64)
+    end = s.nsd_synth_layout(cfg, seed, lo, n, 16, 0, desc.ctypes.data)
+    frames = torch.empty(end + pad, dtype=torch.uint8, device=device)
+    frames[end:].zero_()
+    offs, caps = desc_off(desc), desc_caplen(desc)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        lo_b = int(offs[a])
+        hi_b = int(offs[b - 1] + caps[b - 1])
+        host = np.zeros(hi_b - lo_b + pad, dtype=np.uint8)
+        d = desc[a:b] - np.uint64(lo_b)
+        s.nsd_synth_fill(cfg, seed, lo + a, b - a, host.ctypes.data, d.ctypes.data, threads)
+        frames[lo_b:hi_b].copy_(torch.from_numpy(host[:hi_b - lo_b]))
+        if on_chunk is not None:
+            on_chunk(a, host, d)
+        del host
+    dd = torch.from_numpy(desc.view(np.int64)).to(device)
+    return frames, dd, desc
+
+
 def desc_pack(off, caplen):
     return (np.uint64(caplen) << np.uint64(40)) | np.uint64(off)
 
@@ -146,6 +178,10 @@ def oracle():
         lib.nsor_dissect_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                               ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_int]
+        lib.nsor_dissect_batch_text_mt.restype = ctypes.c_uint64
+        lib.nsor_dissect_batch_text_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                   ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_void_p]
         lib.nsor_dissect_batch_text.restype = ctypes.c_uint64
         lib.nsor_dissect_batch_text.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(_Text)]

@@ -1,18 +1,25 @@
 #!/bin/bash
-# Build a variant of libnsdissect.so with extra compile flags into
-# variants/<name>/ (git-ignored; travels to the GPU box with gpurun).
+# Build an experiment variant of libnsdissect.so into variants/<name>/
+# (git-ignored; travels to the GPU box with gpurun).  Tuning knobs come in as
+# -D flags; experiments that change code (e.g. skip a phase to time the
+# rest) are patches (paths csrc/...) applied to a scratch copy of the
+# sources, never switches in the product sources.
 #   tools/build_variant.sh u8 -DNSD_CSUM_U=8
+#   PATCH=/tmp/nop2.patch tools/build_variant.sh nop2
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
 d=variants/$name
-mkdir -p $d
+rm -rf $d && mkdir -p $d/x/a $d/x/include
+cp -r netsniff-ng_amd/csrc $d/x/a/csrc
+cp include/netsniff_dissect.h $d/x/include/
+if [ -n "$PATCH" ]; then patch -s -d $d/x/a -p0 < "$PATCH"; fi
+make -s -C netsniff-ng_amd
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function $*"
-$H -c netsniff-ng_amd/csrc/nsd_kernels.hip -o $d/k.o
+$H -c $d/x/a/csrc/nsd_kernels.hip -o $d/k.o
 objs="$d/k.o"
 for f in nsd_bpf nsd_host nsd_pipe nsd_format nsd_lookup nsd_pcap; do
-  [ netsniff-ng_amd/build/$f.o -nt netsniff-ng_amd/csrc/$f.cpp ] || [ netsniff-ng_amd/build/$f.o -nt netsniff-ng_amd/csrc/$f.hip ] || make -s -C netsniff-ng_amd
   objs="$objs netsniff-ng_amd/build/$f.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libnsdissect.so $objs
-rm -f $d/k.o
+rm -rf $d/k.o $d/x
