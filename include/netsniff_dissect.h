@@ -10,8 +10,8 @@
  *        dissector_entry_point     <- dissector.h:119 / dissector.c:64-122
  *        dissector_cleanup_all     <- dissector.h:121 / dissector.c:132-138
  *        dissector_set_print_type  <- dissector.h:122 / dissector.c:22-41
- *      The per-packet entry point runs the packet through the HIP kernel
- *      (batch of one) and renders the record with the host formatter.
+ *        struct protocol / pkt_buff and the protos.h ops objects
+ *      The per-packet entry point runs on the host CPU.
  *
  *   2. The batch extension (new): a packed batch of frames is
  *      walked by hand-written CDNA4 kernels, one lane per packet, producing
@@ -180,13 +180,74 @@ enum nsd_counter {
 #define NSD_ERR_NOMEM       -4
 #define NSD_ERR_FORMAT      -5
 
-/* ---- reference surface (dissector.h:118-122) ---------------------------- */
+/* ---- reference surface (dissector.h:118-122) ----------------------------
+ * The per-packet entry runs on the host CPU, as SURVEY 8b plans it (one
+ * packet per launch would be all launch latency): dissector_main's loop
+ * (dissector.c:43-62) over the ops objects below, whose process() functions
+ * run this library's layer step (nsd_walk.h gen_step, the code the device's
+ * general walk runs) and render that layer's text through the caller's
+ * tprintf.  Batches go to the device (the batch extension further down).
+ *   dissector_init_all(fnttype)  dissector.c:124-130 + dissector_eth.c:64-75
+ *       + dissector_sll.c:100-105: print types of every ops object, the
+ *       802.11 / netlink initialisers when those reference objects are
+ *       linked, and the four name tables from ETCDIRE (NSD_ETCDIRE at build
+ *       time, "/etc/netsniff-ng" by default, or nsd_set_etcdir()).
+ *   dissector_entry_point        dissector.c:64-122 (any frame length)
+ *   dissector_cleanup_all        dissector.c:132-138
+ *   dissector_set_print_type     dissector.c:22-41 */
 struct sockaddr_ll;
 void dissector_init_all(int fnttype);
 void dissector_entry_point(uint8_t *packet, size_t len, int linktype, int mode,
 			   struct sockaddr_ll *sll);
 void dissector_cleanup_all(void);
 int  dissector_set_print_type(void *ptr, int type);
+/* the directory dissector_init_all loads udp.conf / tcp.conf / ether.conf /
+ * oui.conf from (the reference's compile-time ETCDIRE_STRING, lookup.c:20-25);
+ * NULL restores the build default */
+void nsd_set_etcdir(const char *dir);
+
+/* ---- proto-ops objects (proto.h:18-33, pkt_buff.h:15-24, protos.h:6-31) --
+ * Same layouts and names as the reference, so the reference objects that
+ * stay in netsniff-ng's link when this library replaces the Ethernet chain
+ * (dissector_80211.o, dissector_netlink.o, proto_80211_mac_hdr.o and, with
+ * libnl, proto_nlmsg.o / mac80211.o: INTEGRATION.md) find none_ops,
+ * dissector_set_print_type and the proto.h dump helpers here, and their
+ * ieee80211_ops / nlmsg_ops chains run inside dissector_entry_point.
+ * Skipped when the reference's own headers were included first. */
+#ifndef PROTO_H
+struct pkt_buff;
+struct protocol {
+	const unsigned int key;
+	void (*print_full)(struct pkt_buff *pkt);
+	void (*print_less)(struct pkt_buff *pkt);
+	struct protocol *next;
+	void (*process)(struct pkt_buff *pkt);
+};
+void empty(struct pkt_buff *pkt);
+void _hex(uint8_t *ptr, size_t len);
+void hex(struct pkt_buff *pkt);
+void _ascii(uint8_t *ptr, size_t len);
+void ascii(struct pkt_buff *pkt);
+void hex_ascii(struct pkt_buff *pkt);
+#endif
+#ifndef PKT_BUFF_H
+struct pkt_buff {
+	uint8_t *head;
+	uint8_t *data;
+	uint8_t *tail;
+	struct protocol *dissector;
+	uint32_t link_type;
+	struct sockaddr_ll *sll;
+};
+#endif
+#ifndef PROTOS_H
+extern struct protocol arp_ops, ethernet_ops, icmpv4_ops, icmpv6_ops, igmp_ops, ip_auth_ops,
+	ip_esp_ops, ipv4_ops, ipv6_ops, ipv6_dest_opts_ops, ipv6_fragm_ops, ipv6_hop_by_hop_ops,
+	ipv6_in_ipv4_ops, ipv6_mobility_ops, ipv6_no_next_header_ops, ipv6_routing_ops, lldp_ops,
+	none_ops, tcp_ops, udp_ops, dccp_ops, vlan_ops, QinQ_ops, mpls_uc_ops;
+#endif
+extern struct protocol sll_ops;   /* dissector_sll.c:84 */
+
 
 /* ---- batch extension ---------------------------------------------------- */
 
@@ -314,6 +375,15 @@ long nsd_format_batch_sll(const uint8_t *frames, const nsd_desc_t *desc, const n
 int nsd_pipe_submit_sll(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
 			const nsd_desc_t *desc, const nsd_sll_t *sll, uint32_t n, nsd_rec *rec,
 			uint32_t *ext, uint32_t *ext_used, uint64_t *counters, int *status);
+
+/* The per-packet entry's walk alone (no text): one packet -> the record the
+ * device writes for it (a chain that needs the ext form gets its pool
+ * entry at word 0 of ext, record slot 0, when ext_words allows; else
+ * NSD_F_OVERFLOW); counters (may be NULL) accumulate.  Host CPU, the same
+ * layer step as the device's general walk. */
+int nsd_walk_packet_cpu(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+			const nsd_sll_t *sll, nsd_rec *rec, uint32_t *ext, uint32_t ext_words,
+			uint64_t *counters);
 
 /* ---- pcap replay front end (`netsniff-ng --in f.pcap`, read_pcap
  * netsniff-ng.c:640-770; pcap_io.h / pcap_sg.c record formats) ---------------

@@ -927,6 +927,68 @@ static void dump_hex(Out &o, const Frame &f, uint32_t from, uint32_t len)
 
 static bool is_lt(int lt, uint32_t v) { return (uint32_t)lt == v || (uint32_t)lt == __builtin_bswap32(v); }
 
+// The print function of ops L.id over [L.start, L.tail): its text, and where
+// the reference parser leaves the cursor (Done)
+static Done render_one(Out &o, const Frame &f, const Layer &L, int mode, uint16_t ip_csum, bool icmp_bad,
+		       const nsd_sll_t *sll)
+{
+	switch (L.id) {
+	case NSD_OPS_ETHERNET:       return r_ethernet(o, f, L, mode);
+	case NSD_OPS_VLAN:           return r_vlan(o, f, L, mode, false);
+	case NSD_OPS_QINQ:           return r_vlan(o, f, L, mode, true);
+	case NSD_OPS_MPLS_UC:        return r_mpls(o, f, L, mode);
+	case NSD_OPS_IPV4:           return r_ipv4(o, f, L, mode, ip_csum);
+	case NSD_OPS_IPV6:
+	case NSD_OPS_IPV6_IN_IPV4:   return r_ipv6(o, f, L, mode);
+	case NSD_OPS_IPV6_HOP_BY_HOP:return r_v6opts(o, f, L, mode, false);
+	case NSD_OPS_IPV6_DEST_OPTS: return r_v6opts(o, f, L, mode, true);
+	case NSD_OPS_IPV6_ROUTING:   return r_routing(o, f, L, mode);
+	case NSD_OPS_IPV6_FRAGM:     return r_fragm(o, f, L, mode);
+	case NSD_OPS_IP_AUTH:        return r_auth(o, f, L, mode);
+	case NSD_OPS_IP_ESP:         return r_esp(o, f, L, mode);
+	case NSD_OPS_IPV6_NO_NEXT:   return r_nonext(o, L, mode);
+	case NSD_OPS_IPV6_MOBILITY:  return r_mobility(o, f, L, mode);
+	case NSD_OPS_TCP:            return r_tcp(o, f, L, mode);
+	case NSD_OPS_UDP:            return r_udp(o, f, L, mode);
+	case NSD_OPS_ICMPV4:         return r_icmp(o, f, L, mode, icmp_bad);
+	case NSD_OPS_ICMPV6:         return r_icmpv6(o, f, L, mode);
+	// leaves the device classifies and the host renders (NSD_F_HOST)
+	case NSD_OPS_ARP:            return r_arp(o, f, L, mode);
+	case NSD_OPS_LLDP:           return r_lldp(o, f, L, mode);
+	case NSD_OPS_IGMP:           return r_igmp(o, f, L, mode);
+	case NSD_OPS_DCCP:           return r_dccp(o, f, L, mode);
+	case NSD_OPS_SLL:            return r_sll(o, L, mode, sll);
+	}
+	return { L.start, L.tail, false, false };   // 802.11, netlink heads
+}
+
+bool render_layer(std::string &s, const uint8_t *pkt, uint32_t caplen, int id, uint32_t start, uint32_t tail,
+		  int mode, uint16_t ip_csum, bool icmp_bad, const nsd_sll_t *sll, uint32_t &data,
+		  uint32_t &ntail, bool &next)
+{
+	Out o(s);
+	Frame f{ pkt, caplen };
+	Layer L{ id, start, tail };
+	const Done dn = render_one(o, f, L, mode, ip_csum, icmp_bad, sll);
+	data = dn.data;
+	ntail = dn.tail;
+	next = dn.next;
+	return dn.ok;
+}
+
+// proto_none.c: _hex / _ascii over [from, from + len) (empty for len 0)
+void render_hex(std::string &s, const uint8_t *pkt, uint32_t caplen, uint32_t from, uint32_t len)
+{
+	Out o(s);
+	dump_hex(o, Frame{ pkt, caplen }, from, len);
+}
+
+void render_ascii(std::string &s, const uint8_t *pkt, uint32_t caplen, uint32_t from, uint32_t len)
+{
+	Out o(s);
+	dump_ascii(o, Frame{ pkt, caplen }, from, len);
+}
+
 // Render one packet; returns NSD_OK or NSD_ERR_FORMAT (text so far kept).
 int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
 		  const nsd_rec &rec, const uint32_t *ext_pool, const nsd_sll_t *sll)
@@ -980,36 +1042,7 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 		Layer L{ ids[k], offs[k], tail };
 		if (L.start > tail)
 			return NSD_ERR_FORMAT;
-		Done dn;
-		switch (L.id) {
-		case NSD_OPS_ETHERNET:       dn = r_ethernet(o, f, L, mode); break;
-		case NSD_OPS_VLAN:           dn = r_vlan(o, f, L, mode, false); break;
-		case NSD_OPS_QINQ:           dn = r_vlan(o, f, L, mode, true); break;
-		case NSD_OPS_MPLS_UC:        dn = r_mpls(o, f, L, mode); break;
-		case NSD_OPS_IPV4:           dn = r_ipv4(o, f, L, mode, rec.ip_csum); break;
-		case NSD_OPS_IPV6:
-		case NSD_OPS_IPV6_IN_IPV4:   dn = r_ipv6(o, f, L, mode); break;
-		case NSD_OPS_IPV6_HOP_BY_HOP:dn = r_v6opts(o, f, L, mode, false); break;
-		case NSD_OPS_IPV6_DEST_OPTS: dn = r_v6opts(o, f, L, mode, true); break;
-		case NSD_OPS_IPV6_ROUTING:   dn = r_routing(o, f, L, mode); break;
-		case NSD_OPS_IPV6_FRAGM:     dn = r_fragm(o, f, L, mode); break;
-		case NSD_OPS_IP_AUTH:        dn = r_auth(o, f, L, mode); break;
-		case NSD_OPS_IP_ESP:         dn = r_esp(o, f, L, mode); break;
-		case NSD_OPS_IPV6_NO_NEXT:   dn = r_nonext(o, L, mode); break;
-		case NSD_OPS_IPV6_MOBILITY:  dn = r_mobility(o, f, L, mode); break;
-		case NSD_OPS_TCP:            dn = r_tcp(o, f, L, mode); break;
-		case NSD_OPS_UDP:            dn = r_udp(o, f, L, mode); break;
-		case NSD_OPS_ICMPV4:         dn = r_icmp(o, f, L, mode, rec.nflags & NSD_F_ICMP_BAD); break;
-		case NSD_OPS_ICMPV6:         dn = r_icmpv6(o, f, L, mode); break;
-		// leaves the device classifies and the host renders (NSD_F_HOST)
-		case NSD_OPS_ARP:            dn = r_arp(o, f, L, mode); break;
-		case NSD_OPS_LLDP:           dn = r_lldp(o, f, L, mode); break;
-		case NSD_OPS_IGMP:           dn = r_igmp(o, f, L, mode); break;
-		case NSD_OPS_DCCP:           dn = r_dccp(o, f, L, mode); break;
-		case NSD_OPS_SLL:            dn = r_sll(o, L, mode, sll); break;
-		default:
-			dn = { L.start, L.tail, false, false };   // 802.11, netlink heads
-		}
+		const Done dn = render_one(o, f, L, mode, rec.ip_csum, rec.nflags & NSD_F_ICMP_BAD, sll);
 		if (!dn.ok)
 			return NSD_ERR_FORMAT;
 		// consistency with the record: next layer's start / final cursor

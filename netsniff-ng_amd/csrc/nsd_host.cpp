@@ -1,11 +1,8 @@
-// nsd_host.cpp - C ABI of the dissector path (include/netsniff_dissect.h):
-// the reference surface (dissector_init_all / dissector_entry_point /
-// dissector_cleanup_all / dissector_set_print_type, dissector.c:22-138) and
-// the batch extension (nsd_dissect_device / dissector_entry_batch).
-//
-// Every dissection goes through the HIP kernel (nsd_kernels.hip); there is no
-// CPU walk in this library.  If no GPU is usable the calls fail loudly
-// (NSD_ERR_HIP, and dissector_entry_point aborts like the reference's panic()).
+// nsd_host.cpp - C ABI of the batch path (include/netsniff_dissect.h):
+// nsd_dissect_device[_ws|_sll] / dissector_entry_batch[_sll] launch the HIP
+// kernels of nsd_kernels.hip over a batch of frames.  There is no CPU walk
+// behind these entries: without a usable GPU they fail loudly (NSD_ERR_HIP).
+// The reference's per-packet surface lives in nsd_proto.cpp.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -28,52 +25,6 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
 				  void *d_ws, int grid, hipStream_t stream);
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
-
-namespace nsd {
-int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-		  const nsd_rec &rec, const uint32_t *ext_pool, const nsd_sll_t *sll = nullptr);
-void format_post_dump(std::string &s, const uint8_t *pkt, uint32_t caplen, int mode, uint32_t from,
-		      uint32_t to);
-}
-
-// ---- struct protocol surface (proto.h:18-26, dissector.c:22-41) -----------
-struct pkt_buff;
-struct protocol {
-	const unsigned int key;
-	void (*print_full)(struct pkt_buff *pkt);
-	void (*print_less)(struct pkt_buff *pkt);
-	struct protocol *next;
-	void (*process)(struct pkt_buff *pkt);
-};
-
-// The print functions of this library are the record renderer; per-ops
-// entries exist so the process-pointer protocol of dissector_set_print_type
-// carries the print mode exactly as in the reference (dissector_eth.c:17-28).
-static void nsd_render_full(struct pkt_buff *) {}
-static void nsd_render_less(struct pkt_buff *) {}
-static struct protocol g_ethernet_ops = { 0, nsd_render_full, nsd_render_less, nullptr, nullptr };
-
-extern "C" int dissector_set_print_type(void *ptr, int type)
-{
-	for (struct protocol *p = (struct protocol *)ptr; p; p = p->next) {
-		switch (type) {
-		case PRINT_NORM: p->process = p->print_full; break;
-		case PRINT_LESS: p->process = p->print_less; break;
-		default: p->process = nullptr; break;
-		}
-	}
-	return 0;
-}
-
-// parse semantics as selected by the ops' process pointers
-static int parse_mode()
-{
-	if (g_ethernet_ops.process == g_ethernet_ops.print_full && g_ethernet_ops.process)
-		return PRINT_NORM;
-	if (g_ethernet_ops.process == g_ethernet_ops.print_less && g_ethernet_ops.process)
-		return PRINT_LESS;
-	return PRINT_HEX;   // process == NULL: the chain does not run
-}
 
 // ---- device context ----------------------------------------------------
 namespace {
@@ -304,12 +255,6 @@ extern "C" int dissector_entry_batch_sll(const uint8_t *frames, size_t frames_le
 	return ok ? NSD_OK : NSD_ERR_HIP;
 }
 
-// ---- output: the host's tprintf if present, else wrapped stdout ---------
-extern "C" {
-void tprintf(char *msg, ...) __attribute__((weak));
-void tprintf_flush(void) __attribute__((weak));
-}
-
 // __tprintf_flush (tprintf.c:65-103) applied to one flushed buffer
 extern "C" long nsd_tprintf_wrap(const char *in, size_t len, int cols, long *state, char *out,
 				 size_t cap)
@@ -349,92 +294,23 @@ extern "C" long nsd_tprintf_wrap(const char *in, size_t len, int cols, long *sta
 	return (long)o;
 }
 
-namespace {
-long g_line_count = 0;
-
-int tty_cols()
-{
-	struct winsize ts;
-	return ioctl(0, TIOCGWINSZ, &ts) == 0 ? ts.ws_col : 80;   // DEFAULT_TTY_SIZE
-}
-
-void emit(const std::string &s)
-{
-	if (tprintf) {
-		for (size_t i = 0; i < s.size(); i += 256) {
-			size_t k = s.size() - i < 256 ? s.size() - i : 256;
-			tprintf((char *)"%.*s", (int)k, s.data() + i);
-		}
-		if (tprintf_flush)
-			tprintf_flush();
-		return;
-	}
-	std::string w(2 * s.size() + 16, '\0');
-	long k = nsd_tprintf_wrap(s.data(), s.size(), tty_cols(), &g_line_count, &w[0], w.size());
-	if (k > 0)
-		fwrite(w.data(), 1, (size_t)k, stdout);
-	fflush(stdout);
-}
-} // namespace
-
-// ---- reference surface ---------------------------------------------------
-extern "C" void dissector_init_all(int fnttype)
-{
-	dissector_set_print_type(&g_ethernet_ops, fnttype);
-}
-
-extern "C" void dissector_cleanup_all(void)
+// the device context of the host-memory batch entry (dissector_cleanup_all
+// frees it, nsd_proto.cpp)
+extern "C" __attribute__((visibility("hidden"))) void nsd_device_ctx_release(void)
 {
 	DevCtx &c = g_ctx;
 	std::lock_guard<std::mutex> lk(c.mu);
 	if (!c.init)
 		return;
 	(void)hipFree(c.frames); (void)hipFree(c.desc); (void)hipFree(c.rec); (void)hipFree(c.ext);
-	(void)hipFree(c.ext_count); (void)hipFree(c.ws); (void)hipFree(c.dev_ws);
+	(void)hipFree(c.ext_count); (void)hipFree(c.ws); (void)hipFree(c.dev_ws); (void)hipFree(c.sll);
 	c.ws = c.dev_ws = nullptr;
 	c.ws_cap = c.dev_ws_cap = 0;
 	(void)hipStreamDestroy(c.stream);
-	c.frames = nullptr; c.desc = nullptr; c.rec = nullptr; c.ext = nullptr;
-	c.frames_cap = c.desc_cap = c.rec_cap = c.ext_cap = 0;
+	c.frames = nullptr; c.desc = nullptr; c.rec = nullptr; c.ext = nullptr; c.sll = nullptr;
+	c.frames_cap = c.desc_cap = c.rec_cap = c.ext_cap = c.sll_cap = 0;
 	c.ext_count = nullptr; c.counters = nullptr; c.stream = nullptr;
 	c.init = false;
-}
-
-extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype, int mode,
-				      struct sockaddr_ll *sll)
-{
-	if (mode == PRINT_NONE)   // dissector.c:70-71
-		return;
-	if (len > NSD_MAX_CAPLEN) {
-		fprintf(stderr, "netsniff-dissect: frame of %zu bytes exceeds %u\n", len, NSD_MAX_CAPLEN);
-		abort();
-	}
-	const int pm = parse_mode();
-	nsd_desc_t d = NSD_DESC(0, len);
-	nsd_rec rec;
-	uint32_t ext[NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS)];
-	uint32_t used = 0;
-	nsd_sll_t ll;
-	memset(&ll, 0, sizeof(ll));
-	if (sll)
-		memcpy(&ll, sll, sizeof(ll));   // struct sockaddr_ll is the same 20 bytes
-	int rc = dissector_entry_batch_sll(packet, len, &d, &ll, 1, linktype, pm, &rec, ext,
-					   NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS), &used, nullptr);
-	if (rc != NSD_OK) {
-		fprintf(stderr, "netsniff-dissect: device dissection failed (%d)\n", rc);
-		abort();   // like panic() (die.h:46): no CPU fallback
-	}
-	std::string s;
-	if (pm == PRINT_NORM || pm == PRINT_LESS) {
-		nsd::format_packet(s, packet, (uint32_t)len, linktype, pm, rec, ext, &ll);
-		// post-chain dumps run on what the chain left (dissector.c:108-118):
-		// after print_full the exit op already pulled everything
-		if (pm == PRINT_LESS)
-			nsd::format_post_dump(s, packet, (uint32_t)len, mode, rec.data_off, rec.tail_off);
-	} else {
-		nsd::format_packet(s, packet, (uint32_t)len, linktype, mode, rec, ext, &ll);
-	}
-	emit(s);
 }
 
 extern "C" const char *nsd_version(void) { return "netsniff-dissect 0.2 (gfx950)"; }

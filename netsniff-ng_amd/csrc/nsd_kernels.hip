@@ -308,27 +308,6 @@ __device__ __forceinline__ void store_rec(uint4 *rec, uint32_t i, uint4 r)
 	__builtin_nontemporal_store(v, (v4u *)(rec + i));
 }
 
-// record words of a finished walk (layout of nsd_rec)
-__device__ __forceinline__ uint4 pack_record(const WalkOut &w)
-{
-	uint4 r;
-	const uint32_t nf = (w.need_ext ? NSD_N_EXT : w.n) | w.flags;
-	r.x = w.chain;
-	r.y = (w.data & 0xFFFF) | (w.tail << 16);
-	if (w.need_ext) {
-		const uint32_t slot = w.ext_on ? w.slot : 0xFFFFFFFFu;
-		r.z = w.ip_csum | (nf << 16) | ((slot & 0xFF) << 24);
-		r.w = slot >> 8;
-	} else {
-		// layer k start / 2 for k = 1..5 (all even)
-		const uint32_t o1 = (uint32_t)(w.offA >> 16) & 0xFFFF, o2 = (uint32_t)(w.offA >> 32) & 0xFFFF;
-		const uint32_t o3 = (uint32_t)(w.offA >> 48), o4 = w.offB & 0xFFFF, o5 = w.offB >> 16;
-		r.z = w.ip_csum | (nf << 16) | ((o1 >> 1) << 24);
-		r.w = (o2 >> 1) | ((o3 >> 1) << 8) | ((o4 >> 1) << 16) | ((o5 >> 1) << 24);
-	}
-	return r;
-}
-
 // Per-wave flag counters: wave-uniform (ballot + popcount, scalar registers);
 // only the byte count is per lane.
 struct FlagCnt {
@@ -558,14 +537,7 @@ __device__ __forceinline__ void sll_head(Shared &sh, WalkOut &w, const uint32_t 
 	w.chain = NSD_OPS_SLL;
 	w.n = 1;
 	atomicAdd(&sh.cnt[NSD_CNT_OPS + NSD_OPS_SLL], 1ull);
-	int nx = 0;
-	if (MODE == PRINT_NORM) {
-		const bool eth = hatype == 1 || hatype == 768 || hatype == 769 || hatype == 772 || hatype == 776 ||
-				 hatype == 777 || hatype == 778 || hatype == 823;
-		const uint32_t e2 = sh.step[32 + NSD_L2H(proto)];
-		nx = eth ? ((e2 & 0xFFFF) == proto ? (int)(e2 >> 16) : 0) : hatype == 824 ? NSD_OPS_NLMSG : 0;
-	}
-	w.id = nx;
+	w.id = sll_next(hatype, proto, MODE, sh.step[32 + NSD_L2H(proto)]);
 }
 
 // The packets pass 1 queued (the block's own queue region), walked with the

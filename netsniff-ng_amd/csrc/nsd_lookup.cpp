@@ -4,6 +4,7 @@
 // the same id shadows an earlier one (lookup.c:84-88 prepends, :130-138
 // returns the first match).  Ports / ether types: direct 64 Ki tables;
 // OUI: sorted vector + binary search.
+#include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -102,6 +103,26 @@ extern "C" void nsd_lookup_cleanup(void)
 	nsd::t_tcp.clear();
 	nsd::t_eth.clear();
 	nsd::t_oui.clear();
+}
+
+// dissector_init_ethernet's four lookup_init calls (dissector_eth.c:71-74,
+// lookup.c:33-56): a missing file leaves its table empty, with the
+// reference's message on stderr
+int nsd::lookup_init_reporting(const char *dir)
+{
+	static const char *files[4] = { "udp.conf", "tcp.conf", "ether.conf", "oui.conf" };
+	int n = 0;
+	nsd_lookup_cleanup();
+	for (int i = 0; i < 4; i++) {
+		const std::string path = std::string(dir ? dir : "") + "/" + files[i];
+		errno = 0;
+		if (nsd::load(path, i))
+			n++;
+		else
+			fprintf(stderr, "Cannot open %s: %s.Port name resolution won't be available.\n", path.c_str(),
+				strerror(errno ? errno : ENOENT));
+	}
+	return n;
 }
 
 extern "C" int nsd_lookup_init(const char *dir)

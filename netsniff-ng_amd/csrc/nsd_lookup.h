@@ -8,4 +8,6 @@ const char *lookup_port_udp(uint32_t id);
 const char *lookup_port_tcp(uint32_t id);
 const char *lookup_ether_type(uint32_t id);
 const char *lookup_vendor(uint32_t id);
+// load the four tables from dir as dissector_init_all does (messages on stderr)
+int lookup_init_reporting(const char *dir);
 }

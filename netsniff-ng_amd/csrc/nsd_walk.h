@@ -8,16 +8,24 @@
 // ICMPv4 checksum, IPv4 tail trim) and looks up the next ops by key.
 // References are given per layer (file:line of the reference parser).
 //
-// The byte source is a template parameter (Src) so the same walk runs over an
-// LDS-staged header window with a global-memory fallback.
+// The byte source (Src) and the sink for what a layer records (Sink) are
+// template parameters, so the same layer step runs
+//   * on the device over an LDS-staged header window (pass 2 of
+//     nsd_kernels.hip: wave-level sinks, ballots, LDS counters), and
+//   * on the host over the whole frame (nsd_cpu.hip: the per-packet entry
+//     point dissector_entry_point and the exported proto-ops objects, which
+//     SURVEY 8b keeps on the CPU: one packet per call is all launch latency).
 #pragma once
 #include <stdint.h>
+#include <hip/hip_runtime.h>
 #include "../../include/netsniff_dissect.h"
+
+#define NSD_HD __host__ __device__ __forceinline__
 
 namespace nsd {
 
 // dissector_eth.c:30-39 (eth_lay2): exact-key map -> ops id
-__device__ __forceinline__ int lay2(uint32_t key)
+NSD_HD int lay2(uint32_t key)
 {
 	switch (key) {
 	case 0x0806: return NSD_OPS_ARP;
@@ -31,22 +39,25 @@ __device__ __forceinline__ int lay2(uint32_t key)
 	return 0;
 }
 
-// dissector_eth.c:44-60 (eth_lay3) as a 256-entry table in constant memory
-__constant__ uint8_t c_lay3[256] = {
-	/*   0 */ NSD_OPS_IPV6_HOP_BY_HOP, NSD_OPS_ICMPV4, NSD_OPS_IGMP, 0, 0, 0, NSD_OPS_TCP, 0,
-	/*   8 */ 0, 0, 0, 0, 0, 0, 0, 0,
-	/*  16 */ 0, NSD_OPS_UDP, 0, 0, 0, 0, 0, 0,
-	/*  24 */ 0, 0, 0, 0, 0, 0, 0, 0,
-	/*  32 */ 0, NSD_OPS_DCCP, 0, 0, 0, 0, 0, 0,
-	/*  40 */ 0, NSD_OPS_IPV6_IN_IPV4, 0, NSD_OPS_IPV6_ROUTING, NSD_OPS_IPV6_FRAGM, 0, 0, 0,
-	/*  48 */ 0, 0, NSD_OPS_IP_ESP, NSD_OPS_IP_AUTH, 0, 0, 0, 0,
-	/*  56 */ 0, 0, NSD_OPS_ICMPV6, NSD_OPS_IPV6_NO_NEXT, NSD_OPS_IPV6_DEST_OPTS, 0, 0, 0,
-	/*  64 */ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-	/*  80 */ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-	/*  96 */ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-	/* 112 */ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-	/* 128 */ 0, 0, 0, 0, 0, 0, 0, NSD_OPS_IPV6_MOBILITY, 0, 0, 0, 0, 0, 0, 0, 0,
-};
+// dissector_eth.c:44-60 (eth_lay3) as a 256-entry table: constant memory on
+// the device, a plain array on the host (same initialiser)
+#define NSD_LAY3_TABLE { \
+	/*   0 */ NSD_OPS_IPV6_HOP_BY_HOP, NSD_OPS_ICMPV4, NSD_OPS_IGMP, 0, 0, 0, NSD_OPS_TCP, 0, \
+	/*   8 */ 0, 0, 0, 0, 0, 0, 0, 0, \
+	/*  16 */ 0, NSD_OPS_UDP, 0, 0, 0, 0, 0, 0, \
+	/*  24 */ 0, 0, 0, 0, 0, 0, 0, 0, \
+	/*  32 */ 0, NSD_OPS_DCCP, 0, 0, 0, 0, 0, 0, \
+	/*  40 */ 0, NSD_OPS_IPV6_IN_IPV4, 0, NSD_OPS_IPV6_ROUTING, NSD_OPS_IPV6_FRAGM, 0, 0, 0, \
+	/*  48 */ 0, 0, NSD_OPS_IP_ESP, NSD_OPS_IP_AUTH, 0, 0, 0, 0, \
+	/*  56 */ 0, 0, NSD_OPS_ICMPV6, NSD_OPS_IPV6_NO_NEXT, NSD_OPS_IPV6_DEST_OPTS, 0, 0, 0, \
+	/*  64 */ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, \
+	/*  80 */ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, \
+	/*  96 */ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, \
+	/* 112 */ 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, \
+	/* 128 */ 0, 0, 0, 0, 0, 0, 0, NSD_OPS_IPV6_MOBILITY, 0, 0, 0, 0, 0, 0, 0, 0, \
+}
+static __constant__ uint8_t c_lay3[256] = NSD_LAY3_TABLE;
+static const uint8_t h_lay3[256] = NSD_LAY3_TABLE;
 
 // the walk looks eth_lay3 up through its byte source (s.lay3(key)), which
 // serves it from an LDS copy of c_lay3: a per-lane constant-memory read would
@@ -83,6 +94,13 @@ struct GenSink {
 	uint32_t *wc;                 // LDS: this wave's chunk {next word, words left}
 	unsigned long long *s_cnt;    // LDS: block counters
 	uint32_t *lay;                // LDS: this wave's layer lists, [j * 64 + lane]
+
+	// wave-uniform branch condition: some lane needs the body
+	__device__ __forceinline__ bool any(bool c) const { return __ballot(c) != 0; }
+	// a chain reaching layer 6 + NSD_LDS_LAYERS takes its pool entry now (rare)
+	__device__ __forceinline__ void take_deep(bool deep_first, WalkOut &w) const;
+	// count layer k (ops id, start offset) and keep it beyond the record
+	__device__ __forceinline__ void layer(const WalkOut &w, uint32_t k, int id, uint32_t start) const;
 };
 
 // Wave-uniform call: every lane with `want` gets a pool entry of `words`
@@ -123,14 +141,57 @@ __device__ __forceinline__ uint32_t ext_take(const GenSink &g, bool want, uint32
 	return want && (uint64_t)s + words <= g.pool_words ? s : 0xFFFFFFFFu;
 }
 
-__device__ __forceinline__ uint16_t off_of(const WalkOut &w, uint32_t k)
+// the sink's layer store: layers 6..15 in the wave's LDS list, deeper ones in
+// the packet's pool entry (taken by take_deep)
+__device__ __forceinline__ void GenSink::layer(const WalkOut &w, uint32_t k, int id, uint32_t start) const
+{
+	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
+	atomicAdd(&s_cnt[NSD_CNT_OPS + id], 1ull);   // the oracle counts the first 64 layers
+	const uint32_t lv = (uint32_t)id | start << 16;
+	if (k >= NSD_REC_MAX_LAYERS && k < DEEP)
+		lay[(k - NSD_REC_MAX_LAYERS) * 64 + __lane_id()] = lv;
+	else if (k >= DEEP && w.slot != 0xFFFFFFFFu)
+		pool[w.slot + NSD_EXT_HDR_WORDS + k] = lv;
+}
+
+__device__ __forceinline__ void GenSink::take_deep(bool deep_first, WalkOut &w) const
+{
+	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
+	if (__ballot(deep_first)) {
+		const uint32_t sb = ext_take(*this, deep_first, NSD_EXT_WORDS(DEEP + 1));
+		if (deep_first) {
+			w.slot = sb;
+			w.ext_on = true;
+		}
+	}
+}
+
+// The host walk's sink: every layer into the caller's arrays (the host
+// keeps the whole chain, so nothing is taken from a pool while walking)
+struct HostSink {
+	uint8_t *ids;                 // [NSD_EXT_MAX_LAYERS]
+	uint16_t *offs;               // [NSD_EXT_MAX_LAYERS]
+	uint64_t *counters;           // NSD_NCOUNTERS, or NULL
+
+	__host__ bool any(bool c) const { return c; }
+	__host__ void take_deep(bool, WalkOut &) const {}
+	__host__ void layer(const WalkOut &, uint32_t k, int id, uint32_t start) const
+	{
+		ids[k] = (uint8_t)id;
+		offs[k] = (uint16_t)start;
+		if (counters)
+			counters[NSD_CNT_OPS + id]++;
+	}
+};
+
+NSD_HD uint16_t off_of(const WalkOut &w, uint32_t k)
 {
 	return k < 4 ? (uint16_t)(w.offA >> (16 * k)) : (uint16_t)(w.offB >> (16 * (k - 4)));
 }
 
 // csum() (csum.h:12-22) over `nwords` little-endian u16 words from `off`
 template <class Src>
-__device__ __forceinline__ uint16_t calc_csum(const Src &s, uint32_t off, uint32_t nwords)
+NSD_HD uint16_t calc_csum(const Src &s, uint32_t off, uint32_t nwords)
 {
 	uint32_t sum = s.sum16(off, nwords);   // <= 32767 words * 0xffff fits in 32 bits
 	sum = (sum >> 16) + (sum & 0xffff);
@@ -139,7 +200,7 @@ __device__ __forceinline__ uint16_t calc_csum(const Src &s, uint32_t off, uint32
 }
 
 // Walk state initialisation (pkt_alloc: data = head, tail = head + len).
-__device__ __forceinline__ void walk_init(WalkOut &w, uint32_t caplen, int start_id)
+NSD_HD void walk_init(WalkOut &w, uint32_t caplen, int start_id)
 {
 	w.data = 0;
 	w.tail = caplen;
@@ -178,32 +239,34 @@ enum : uint32_t {
 };
 #define NSD_STEP(minl, adv, kind, kpos, kw16, need) \
 	((minl) | (adv) << 8 | (kind) << 16 | (kpos) << 20 | (kw16) << 24 | (uint32_t)(need) << 25)
-__constant__ uint32_t c_step[32] = {
-	/*  0 invalid   */ NSD_STEP(0, 0, K_HOST, 0, 0, 0),
-	/*  1 ethernet  */ NSD_STEP(14, 14, K_CONT, 12, 1, 14),   // proto_ethernet.c:48-79
-	/*  2 vlan      */ NSD_STEP(4, 4, K_CONT, 2, 1, 4),       // proto_vlan.c:22-40
-	/*  3 qinq      */ NSD_STEP(4, 4, K_CONT, 2, 1, 4),       // proto_vlan_q_in_q.c:23-41
-	/*  4 mpls      */ NSD_STEP(0, 0, K_MPLS, 0, 0, 16),      // proto_mpls_unicast.c:49-77
-	/*  5 arp       */ NSD_STEP(0, 0, K_HOST, 0, 0, 0),
-	/*  6 lldp      */ NSD_STEP(0, 0, K_HOST, 0, 0, 0),
-	/*  7 ipv4      */ NSD_STEP(20, 20, K_IPV4, 9, 0, 20),    // proto_ipv4.c:34-178
-	/*  8 ipv6      */ NSD_STEP(40, 40, K_CONT, 6, 0, 8),     // proto_ipv6.c:22-105
-	/*  9 ipv6inv4  */ NSD_STEP(40, 40, K_CONT, 6, 0, 8),     // proto_ipv6_in_ipv4.c:20-24
-	/* 10 icmpv4    */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0),       // proto_icmpv4.c:34-51
-	/* 11 icmpv6    */ NSD_STEP(4, 4, K_ICMP6, 0, 0, 4),      // proto_icmpv6.c:1667-1699
-	/* 12 igmp      */ NSD_STEP(0, 0, K_HOST, 0, 0, 0),
-	/* 13 ah        */ NSD_STEP(12, 12, K_AH, 0, 0, 4),       // proto_ip_authentication_hdr.c:26-69
-	/* 14 esp       */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0),       // proto_ip_esp.c:23-35
-	/* 15 destopts  */ NSD_STEP(2, 2, K_T8, 0, 0, 4),         // proto_ipv6_dest_opts.c:40-72
-	/* 16 fragm     */ NSD_STEP(8, 8, K_CONT, 0, 0, 4),       // proto_ipv6_fragm.c:25-47
-	/* 17 hopbyhop  */ NSD_STEP(2, 2, K_T8, 0, 0, 4),         // proto_ipv6_hop_by_hop.c:39-71
-	/* 18 mobility  */ NSD_STEP(6, 6, K_MOB, 0, 0, 4),        // proto_ipv6_mobility_hdr.c:247-309
-	/* 19 nonext    */ NSD_STEP(0, 0, K_LEAF, 0, 0, 0),       // proto_ipv6_no_nxt_hdr.c:17-29
-	/* 20 routing   */ NSD_STEP(4, 4, K_T8, 0, 0, 4),         // proto_ipv6_routing.c:79-122
-	/* 21 tcp       */ NSD_STEP(20, 20, K_LEAF, 0, 0, 0),     // proto_tcp.c:63-107 (options not pulled)
-	/* 22 udp       */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0),       // proto_udp.c:23-58
-	/* 23..31: dccp, none, sll, 802.11, nlmsg, unused: host leaves */
-};
+#define NSD_STEP_TABLE { \
+	/*  0 invalid   */ NSD_STEP(0, 0, K_HOST, 0, 0, 0), \
+	/*  1 ethernet  */ NSD_STEP(14, 14, K_CONT, 12, 1, 14), /* proto_ethernet.c:48-79 */ \
+	/*  2 vlan      */ NSD_STEP(4, 4, K_CONT, 2, 1, 4), /* proto_vlan.c:22-40 */ \
+	/*  3 qinq      */ NSD_STEP(4, 4, K_CONT, 2, 1, 4), /* proto_vlan_q_in_q.c:23-41 */ \
+	/*  4 mpls      */ NSD_STEP(0, 0, K_MPLS, 0, 0, 16), /* proto_mpls_unicast.c:49-77 */ \
+	/*  5 arp       */ NSD_STEP(0, 0, K_HOST, 0, 0, 0), \
+	/*  6 lldp      */ NSD_STEP(0, 0, K_HOST, 0, 0, 0), \
+	/*  7 ipv4      */ NSD_STEP(20, 20, K_IPV4, 9, 0, 20), /* proto_ipv4.c:34-178 */ \
+	/*  8 ipv6      */ NSD_STEP(40, 40, K_CONT, 6, 0, 8), /* proto_ipv6.c:22-105 */ \
+	/*  9 ipv6inv4  */ NSD_STEP(40, 40, K_CONT, 6, 0, 8), /* proto_ipv6_in_ipv4.c:20-24 */ \
+	/* 10 icmpv4    */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0), /* proto_icmpv4.c:34-51 */ \
+	/* 11 icmpv6    */ NSD_STEP(4, 4, K_ICMP6, 0, 0, 4), /* proto_icmpv6.c:1667-1699 */ \
+	/* 12 igmp      */ NSD_STEP(0, 0, K_HOST, 0, 0, 0), \
+	/* 13 ah        */ NSD_STEP(12, 12, K_AH, 0, 0, 4), /* proto_ip_authentication_hdr.c:26-69 */ \
+	/* 14 esp       */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0), /* proto_ip_esp.c:23-35 */ \
+	/* 15 destopts  */ NSD_STEP(2, 2, K_T8, 0, 0, 4), /* proto_ipv6_dest_opts.c:40-72 */ \
+	/* 16 fragm     */ NSD_STEP(8, 8, K_CONT, 0, 0, 4), /* proto_ipv6_fragm.c:25-47 */ \
+	/* 17 hopbyhop  */ NSD_STEP(2, 2, K_T8, 0, 0, 4), /* proto_ipv6_hop_by_hop.c:39-71 */ \
+	/* 18 mobility  */ NSD_STEP(6, 6, K_MOB, 0, 0, 4), /* proto_ipv6_mobility_hdr.c:247-309 */ \
+	/* 19 nonext    */ NSD_STEP(0, 0, K_LEAF, 0, 0, 0), /* proto_ipv6_no_nxt_hdr.c:17-29 */ \
+	/* 20 routing   */ NSD_STEP(4, 4, K_T8, 0, 0, 4), /* proto_ipv6_routing.c:79-122 */ \
+	/* 21 tcp       */ NSD_STEP(20, 20, K_LEAF, 0, 0, 0), /* proto_tcp.c:63-107 (options not pulled) */ \
+	/* 22 udp       */ NSD_STEP(8, 8, K_LEAF, 0, 0, 0), /* proto_udp.c:23-58 */ \
+	/* 23..31: dccp, none, sll, 802.11, nlmsg, unused: host leaves */ \
+}
+static __constant__ uint32_t c_step[32] = NSD_STEP_TABLE;
+static const uint32_t h_step[32] = NSD_STEP_TABLE;
 
 // eth_lay2 (dissector_eth.c:30-39) as a 32-entry perfect hash for the
 // general walk: slot ((key * 0x156) & 0xFFFF) >> 11 holds key | ops << 16
@@ -223,7 +286,44 @@ struct Lay2Hash {
 };
 static_assert(NSD_L2H(0x0806) != NSD_L2H(0x88cc) && NSD_L2H(0x8100) != NSD_L2H(0x0800) &&
 	      NSD_L2H(0x86DD) != NSD_L2H(0x88a8), "eth_lay2 hash must be perfect");
-__constant__ Lay2Hash c_lay2h;
+static __constant__ Lay2Hash c_lay2h;
+static constexpr Lay2Hash h_lay2h;
+
+// record words of a finished walk (layout of nsd_rec)
+NSD_HD uint4 pack_record(const WalkOut &w)
+{
+	uint4 r;
+	const uint32_t nf = (w.need_ext ? NSD_N_EXT : w.n) | w.flags;
+	r.x = w.chain;
+	r.y = (w.data & 0xFFFF) | (w.tail << 16);
+	if (w.need_ext) {
+		const uint32_t slot = w.ext_on ? w.slot : 0xFFFFFFFFu;
+		r.z = w.ip_csum | (nf << 16) | ((slot & 0xFF) << 24);
+		r.w = slot >> 8;
+	} else {
+		// layer k start / 2 for k = 1..5 (all even)
+		const uint32_t o1 = (uint32_t)(w.offA >> 16) & 0xFFFF, o2 = (uint32_t)(w.offA >> 32) & 0xFFFF;
+		const uint32_t o3 = (uint32_t)(w.offA >> 48), o4 = w.offB & 0xFFFF, o5 = w.offB >> 16;
+		r.z = w.ip_csum | (nf << 16) | ((o1 >> 1) << 24);
+		r.w = (o2 >> 1) | ((o3 >> 1) << 8) | ((o4 >> 1) << 16) | ((o5 >> 1) << 24);
+	}
+	return r;
+}
+
+// The LINKTYPE_LINUX_SLL head's next ops (dissector_sll.c:39-82): in
+// print_full a hatype that pcap_devtype_to_linktype (pcap_io.h:205-267) maps
+// to LINKTYPE_EN10MB continues in eth_lay2 with ntohs(sll_protocol),
+// ARPHRD_NETLINK continues with the netlink ops (a host leaf), anything else
+// ends the chain; print_less dispatches nothing.  e2 = the eth_lay2 hash
+// entry at NSD_L2H(proto).
+NSD_HD int sll_next(uint32_t hatype, uint32_t proto, int mode, uint32_t e2)
+{
+	if (mode != PRINT_NORM)
+		return 0;
+	const bool eth = hatype == 1 || hatype == 768 || hatype == 769 || hatype == 772 || hatype == 776 ||
+			 hatype == 777 || hatype == 778 || hatype == 823;
+	return eth ? ((e2 & 0xFFFF) == proto ? (int)(e2 >> 16) : 0) : hatype == 824 ? NSD_OPS_NLMSG : 0;
+}
 
 // get_mh_type's subtype pull sizes for mobility types 0..7
 // (proto_ipv6_mobility_hdr.c:206-245), one byte per type
@@ -240,8 +340,8 @@ __constant__ Lay2Hash c_lay2h;
 // layer: record the ops (chain word / offsets, or the ext pool entry once
 // the chain needs the ext form), count it, advance the pkt_buff cursor
 // exactly as the reference parser does, look up the next ops.
-template <int MODE, class Src>
-__device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, const GenSink &g)
+template <int MODE, class Src, class Sink>
+NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 {
 	const int id = act ? w.id : 0;
 	const uint32_t start = w.data;
@@ -250,29 +350,15 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 	// layer past byte 510, forces the ext form
 	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
 	const bool need_now = act && (k >= NSD_REC_MAX_LAYERS || (k >= 1 && start > 510));
-	const bool deep_first = act && k == DEEP && !w.ext_on;
-	if (__ballot(deep_first)) {
-		// a chain this deep takes its pool entry now (rare)
-		const uint32_t sb = ext_take(g, deep_first, NSD_EXT_WORDS(DEEP + 1));
-		if (deep_first) {
-			w.slot = sb;
-			w.ext_on = true;
-		}
-	}
+	g.take_deep(act && k == DEEP && !w.ext_on, w);
 	const uint32_t kk = k < 8 ? k : 7;   // keeps the shifts below defined
 	w.need_ext = w.need_ext || need_now;
 	w.chain |= act && k < NSD_REC_MAX_LAYERS ? (uint32_t)id << (5 * kk) : 0u;
 	w.offA |= act && k < 4 ? (uint64_t)(start & 0xFFFF) << (16 * (kk & 3)) : 0ull;
 	w.offB |= act && k >= 4 && k < NSD_REC_MAX_LAYERS ? (start & 0xFFFF) << (16 * (kk & 1)) : 0u;
 	w.flags |= act && k >= NSD_EXT_MAX_LAYERS ? NSD_F_OVERFLOW : 0;
-	if (act && k < NSD_EXT_MAX_LAYERS) {
-		atomicAdd(&g.s_cnt[NSD_CNT_OPS + id], 1ull);   // the oracle counts the first 64 layers
-		const uint32_t lv = (uint32_t)id | start << 16;
-		if (k >= NSD_REC_MAX_LAYERS && k < DEEP)
-			g.lay[(k - NSD_REC_MAX_LAYERS) * 64 + __lane_id()] = lv;
-		else if (k >= DEEP && w.slot != 0xFFFFFFFFu)
-			g.pool[w.slot + NSD_EXT_HDR_WORDS + k] = lv;
-	}
+	if (act && k < NSD_EXT_MAX_LAYERS)
+		g.layer(w, k, id, start);
 	w.n = act ? k + 1 : k;
 
 	// ---- parse (bytes >= caplen read as zero).  Everything below is
@@ -343,13 +429,13 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 	}
 	// ---- the rare heavy bodies, behind wave-uniform branches
 	const bool v4 = upd && kind == K_IPV4 && pulled;
-	if (MODE == PRINT_NORM && __ballot(v4)) {
+	if (MODE == PRINT_NORM && g.any(v4)) {
 		// checksum over ihl*4 bytes, past the frame too (bytes >= caplen are 0)
 		if (v4)
 			w.ip_csum = calc_csum(s, start, ihl * 2u);
 	}
 	const bool i4 = upd && id == NSD_OPS_ICMPV4 && pulled;
-	if (MODE == PRINT_NORM && __ballot(i4)) {
+	if (MODE == PRINT_NORM && g.any(i4)) {
 		// calc_csum(icmp, pkt_len + 8): the whole (post-trim) message, odd
 		// trailing byte dropped (csum.h:24-27); past the window: pending
 		if (i4) {
@@ -364,7 +450,7 @@ __device__ __forceinline__ void gen_step(const Src &s, bool act, WalkOut &w, con
 		}
 	}
 	const bool mp = act && kind == K_MPLS;
-	if (__ballot(mp)) {                           // proto_mpls_unicast.c:49-77
+	if (g.any(mp)) {                              // proto_mpls_unicast.c:49-77
 		if (mp) {
 			uint32_t d = start, l = len;
 			bool ok = true;

@@ -71,7 +71,7 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_replay_pcap", "nsd_t3_block_desc", "nsd_dissect_device_sll",
                "dissector_entry_batch_sll", "nsd_format_packet_sll", "nsd_format_batch_sll",
                "nsd_pipe_submit_sll", "nsd_pcap_read_batch_sll", "nsd_t3_block_desc_sll",
-               "nsd_replay_pcap_out", "nsd_build_info"]
+               "nsd_replay_pcap_out", "nsd_build_info", "nsd_walk_packet_cpu", "nsd_set_etcdir"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -180,6 +180,10 @@ def lib():
         L.nsd_pcap_read_batch_sll.argtypes = [_vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp]
         L.nsd_pipe_submit_sll.restype = _int
         L.nsd_pipe_submit_sll.argtypes = [_vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
+        L.nsd_walk_packet_cpu.restype = _int
+        L.nsd_walk_packet_cpu.argtypes = [_vp, _u32, _int, _int, _vp, _vp, _vp, _u32, _vp]
+        L.nsd_set_etcdir.restype = None
+        L.nsd_set_etcdir.argtypes = [ctypes.c_char_p]
         L.nsd_replay_pcap.restype = ctypes.c_long
         L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp, _int]
         _lib = L
@@ -251,6 +255,34 @@ def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_wor
                                          used.ctypes.data, counters.ctypes.data)
     _check(rc, "dissector_entry_batch")
     return rec, ext[:min(int(used[0]), ext_words)], counters
+
+
+def walk_cpu(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, sll=None):
+    """The per-packet entry point's walk (host CPU, nsd_walk_packet_cpu) over
+    every packet of a host batch: (records, {packet: (ids, offs)} of the ext
+    chains, counters).  The batch path is nsd_dissect_device / entry_batch."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    desc = np.ascontiguousarray(desc, dtype=np.uint64)
+    sll = None if sll is None else np.ascontiguousarray(sll, dtype=SLL_DTYPE)
+    n = len(desc)
+    rec = np.zeros(n, dtype=REC_DTYPE)
+    cnt = np.zeros(NCOUNTERS, dtype=np.uint64)
+    ext = np.zeros(ext_words(EXT_MAX_LAYERS), dtype=np.uint32)
+    chains = {}
+    L = lib()
+    base = frames.ctypes.data
+    for i in range(n):
+        d = int(desc[i])
+        off, cl = d & 0xFFFFFFFFFF, d >> 40
+        r = rec[i:i + 1]
+        rc = L.nsd_walk_packet_cpu(base + off, cl, linktype, mode,
+                                   None if sll is None else sll[i:i + 1].ctypes.data,
+                                   r.ctypes.data, ext.ctypes.data, len(ext), cnt.ctypes.data)
+        _check(rc, "nsd_walk_packet_cpu")
+        if (int(r[0]["nflags"]) & 7) == 7 and not (int(r[0]["nflags"]) & 0x20):
+            _, ids, offs = ext_entry(ext, 0)
+            chains[i] = (ids, offs)
+    return rec, chains, cnt
 
 
 class Pipe:

@@ -18,7 +18,7 @@ make -s -C netsniff-ng_amd
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function $*"
 $H -c $d/x/a/csrc/nsd_kernels.hip -o $d/k.o
 objs="$d/k.o"
-for f in nsd_bpf nsd_host nsd_pipe nsd_format nsd_lookup nsd_pcap; do
+for f in nsd_bpf nsd_cpu nsd_host nsd_pipe nsd_format nsd_lookup nsd_pcap nsd_proto; do
   objs="$objs netsniff-ng_amd/build/$f.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $d/libnsdissect.so $objs
