@@ -1,0 +1,46 @@
+"""kbench.py - development timing of the dissect kernel alone: K launches over
+one resident synthetic batch per config, kernel ms from HIP events (no
+result checks: experiment variants that skip a phase run through it too).
+Not the benchmark (bench.py is).
+
+  python tools/kbench.py --configs udp64,imix,ipv6x --steps 10 [--lib path]
+"""
+import argparse
+import os
+import shutil
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "netsniff-ng_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="udp64,imix,ipv6x")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--packets", type=int, default=1 << 24)
+    ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--grid", type=int, default=0)
+    args = ap.parse_args()
+    import bench
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    for key in args.configs.split(","):
+        b = bench.Batch(key, args.packets, 0, 1, dev)
+        ms = bench.time_steps(b, args.mode, args.steps, args.warmup, args.grid)
+        cnt = b.counters.cpu().numpy().view(np.uint64)
+        r = b.roofline(ms)
+        print(f"{key:6s} kernel_ms={ms:.4f} frac={r['frac'] if r else None} read_frac={r['read_frac'] if r else None}"
+              f" pkts_counted={int(cnt[32])}", flush=True)
+        b.free()
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
