@@ -15,6 +15,8 @@
 // frame bytes the program reads (for header filters: the first 64-B line),
 // the 4-B verdict; the compaction adds 12 B read + 8 B per accepted packet.
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -302,6 +304,15 @@ struct nsd_bpf_prog {
 	uint32_t len = 0;
 	uint32_t usesmem = 0;
 	uint2 *d_prog = nullptr;   // decoded program, device memory
+	// nsd_bpf_filter_batch's device buffers, kept and grown across calls (a
+	// hipFree per batch would synchronise the device under the replay's
+	// pipelined batches)
+	std::mutex mu;
+	uint8_t *d_frames = nullptr;
+	size_t frames_cap = 0;
+	uint64_t *d_desc = nullptr;
+	uint32_t *d_verdict = nullptr;
+	size_t n_cap = 0;
 };
 
 static bool hip_ok(hipError_t e, const char *what)
@@ -405,6 +416,12 @@ extern "C" void nsd_bpf_free(nsd_bpf_prog *prog)
 		return;
 	if (prog->d_prog)
 		(void)hipFree(prog->d_prog);
+	if (prog->d_frames)
+		(void)hipFree(prog->d_frames);
+	if (prog->d_desc)
+		(void)hipFree(prog->d_desc);
+	if (prog->d_verdict)
+		(void)hipFree(prog->d_verdict);
 	delete prog;
 }
 
@@ -455,20 +472,38 @@ extern "C" int nsd_bpf_filter_batch(const nsd_bpf_prog *prog, const uint8_t *fra
 	for (uint32_t i = 0; i < n; i++)
 		if (NSD_DESC_OFF(desc[i]) + NSD_DESC_CAPLEN(desc[i]) > frames_len)
 			return NSD_ERR_ARG;
-	uint8_t *d_frames = nullptr;
-	uint64_t *d_desc = nullptr;
-	uint32_t *d_verdict = nullptr;
-	bool ok = hip_ok(hipMalloc(&d_frames, frames_len + NSD_FRAME_PAD), "hipMalloc") &&
-		  hip_ok(hipMalloc(&d_desc, (size_t)n * 8), "hipMalloc") &&
-		  hip_ok(hipMalloc(&d_verdict, (size_t)n * 4), "hipMalloc") &&
-		  hip_ok(hipMemcpy(d_frames, frames, frames_len, hipMemcpyHostToDevice), "H2D") &&
-		  hip_ok(hipMemset(d_frames + frames_len, 0, NSD_FRAME_PAD), "memset") &&
-		  hip_ok(hipMemcpy(d_desc, desc, (size_t)n * 8, hipMemcpyHostToDevice), "H2D");
-	ok = ok && nsd_bpf_filter_device(prog, d_frames, d_desc, n, d_verdict, nullptr, nullptr, nullptr,
-					 nullptr) == NSD_OK;
-	ok = ok && hip_ok(hipMemcpy(verdict, d_verdict, (size_t)n * 4, hipMemcpyDeviceToHost), "D2H");
-	if (d_frames) (void)hipFree(d_frames);
-	if (d_desc) (void)hipFree(d_desc);
-	if (d_verdict) (void)hipFree(d_verdict);
+	nsd_bpf_prog *h = const_cast<nsd_bpf_prog *>(prog);
+	std::lock_guard<std::mutex> lk(h->mu);
+	bool ok = true;
+	if (frames_len + NSD_FRAME_PAD > h->frames_cap) {
+		if (h->d_frames)
+			(void)hipFree(h->d_frames);
+		h->d_frames = nullptr;
+		h->frames_cap = 0;
+		const size_t want = frames_len + frames_len / 4 + NSD_FRAME_PAD;
+		ok = hip_ok(hipMalloc(&h->d_frames, want), "hipMalloc");
+		if (ok)
+			h->frames_cap = want;
+	}
+	if (ok && n > h->n_cap) {
+		if (h->d_desc)
+			(void)hipFree(h->d_desc);
+		if (h->d_verdict)
+			(void)hipFree(h->d_verdict);
+		h->d_desc = nullptr;
+		h->d_verdict = nullptr;
+		h->n_cap = 0;
+		const size_t want = n + n / 4 + 64;
+		ok = hip_ok(hipMalloc(&h->d_desc, want * 8), "hipMalloc") &&
+		     hip_ok(hipMalloc(&h->d_verdict, want * 4), "hipMalloc");
+		if (ok)
+			h->n_cap = want;
+	}
+	ok = ok && hip_ok(hipMemcpy(h->d_frames, frames, frames_len, hipMemcpyHostToDevice), "H2D") &&
+	     hip_ok(hipMemset(h->d_frames + frames_len, 0, NSD_FRAME_PAD), "memset") &&
+	     hip_ok(hipMemcpy(h->d_desc, desc, (size_t)n * 8, hipMemcpyHostToDevice), "H2D");
+	ok = ok && nsd_bpf_filter_device(prog, h->d_frames, (const nsd_desc_t *)h->d_desc, n, h->d_verdict, nullptr,
+					 nullptr, nullptr, nullptr) == NSD_OK;
+	ok = ok && hip_ok(hipMemcpy(verdict, h->d_verdict, (size_t)n * 4, hipMemcpyDeviceToHost), "D2H");
 	return ok ? NSD_OK : NSD_ERR_HIP;
 }

@@ -89,6 +89,9 @@ static void walk_packet(const uint8_t *pkt, uint32_t caplen, int start_id, const
 // returns the next ops (0: the chain ends) and the new cursor, the IPv4
 // header checksum and the NSD_F_* flags the layer raised.  The SLL head
 // reads only sll (pkt->sll).
+void cpu_count_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode, const nsd_sll_t *sll,
+		      uint64_t *counters);
+
 int cpu_step(int mode, const uint8_t *pkt, uint32_t caplen, int id, uint32_t &data, uint32_t &tail,
 	     uint16_t &ip_csum, uint8_t &flags, const nsd_sll_t *sll)
 {
@@ -121,6 +124,28 @@ int cpu_step(int mode, const uint8_t *pkt, uint32_t caplen, int id, uint32_t &da
 } // namespace nsd
 
 __attribute__((visibility("hidden"))) int nsd_start_for(int linktype);   // nsd_host.cpp
+
+// The counters the device adds for one packet, from the host walk, for frames
+// the batch path cannot carry (caplen above NSD_MAX_CAPLEN: the pcap replay
+// renders those through the per-packet path)
+void nsd::cpu_count_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode, const nsd_sll_t *sll,
+			   uint64_t *counters)
+{
+	WalkOut w;
+	uint8_t ids[NSD_EXT_MAX_LAYERS];
+	uint16_t offs[NSD_EXT_MAX_LAYERS];
+	if (mode == PRINT_NORM || mode == PRINT_LESS) {
+		const int start = nsd_start_for(linktype);
+		if (mode == PRINT_NORM)
+			walk_packet<PRINT_NORM>(pkt, caplen, start, sll, w, ids, offs, counters);
+		else
+			walk_packet<PRINT_LESS>(pkt, caplen, start, sll, w, ids, offs, counters);
+		count_flags(counters, w, caplen);
+	} else {
+		counters[NSD_CNT_PKTS]++;
+		counters[NSD_CNT_BYTES] += caplen;
+	}
+}
 
 // One packet through the host walk: the record the device writes for it; a
 // chain that needs the ext form gets its entry at word 0 of ext (its

@@ -17,7 +17,12 @@
 //     (pcap_get_length :322-352);
 //   - a record with caplen 0 or above the 1 MiB replay buffer ends the
 //     replay, as pcap_sg_read's -EINVAL does (pcap_sg.c:121-123), and so
-//     does a short read at the end of the file.
+//     does a short read at the end of the file;
+//   - a record longer than a batch can carry (NSD_MAX_CAPLEN < caplen <=
+//     1 MiB: tcpdump's default snaplen is 262144, GRO frames are long) ends
+//     the batch before it; the batch reader reports NSD_ERR_CAPLEN when it
+//     is the next record, and the replay dissects it through the per-packet
+//     path (nsd_proto.cpp), in file order.
 #include <errno.h>
 #include <fcntl.h>
 #include <stdint.h>
@@ -31,6 +36,13 @@
 #include <vector>
 
 #include "../../include/netsniff_dissect.h"
+
+namespace nsd {
+void render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
+		       const nsd_sll_t *sll);
+void cpu_count_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode, const nsd_sll_t *sll,
+		      uint64_t *counters);
+}
 
 namespace {
 
@@ -196,8 +208,13 @@ static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *des
 			wl = bswap32(wl);
 		}
 		const uint32_t caplen = cl - p->ll_extra;   // unsigned, as the reference computes it
-		if (caplen == 0 || caplen > REPLAY_BUF || caplen > NSD_MAX_CAPLEN) {
+		if (caplen == 0 || caplen > REPLAY_BUF) {
 			p->eof = true;   // pcap_sg_read: -EINVAL ends read_pcap's loop
+			break;
+		}
+		if (caplen > NSD_MAX_CAPLEN) {
+			if (n == 0)
+				return NSD_ERR_CAPLEN;   // the next record does not fit a batch
 			break;
 		}
 		const size_t at = (off + 15) & ~(size_t)15;
@@ -240,6 +257,46 @@ static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *des
 	return n;
 }
 
+// The next record whatever its length (<= the 1 MiB replay buffer), for the
+// records a batch cannot carry: its bytes into `frame`, its header as stored
+// into rhdr (may be NULL), its cooked header into *sll.  Returns caplen, 0 at
+// the end of the replay.
+static long read_one(nsd_pcap *p, std::vector<uint8_t> &frame, nsd_sll_t *sll, uint8_t *rhdr)
+{
+	if (p->eof || !p->fill(p->hdrsize)) {
+		p->eof = true;
+		return 0;
+	}
+	const uint8_t *h = p->buf.data() + p->pos;
+	uint32_t cl;
+	memcpy(&cl, h + 8, 4);
+	if (p->swapped)
+		cl = bswap32(cl);
+	const uint32_t caplen = cl - p->ll_extra;
+	if (caplen == 0 || caplen > REPLAY_BUF || !p->fill((size_t)p->hdrsize + caplen)) {
+		p->eof = true;
+		return 0;
+	}
+	h = p->buf.data() + p->pos;
+	frame.assign(h + p->hdrsize, h + p->hdrsize + caplen);
+	frame.resize((size_t)caplen + NSD_FRAME_PAD, 0);
+	if (rhdr)
+		memcpy(rhdr, h, p->hdrsize);
+	nsd_sll_t ll;
+	memset(&ll, 0, sizeof(ll));
+	if (p->ll_extra) {
+		const uint8_t *c = h + 16;
+		ll.pkttype = (uint8_t)(((uint32_t)c[0] << 8) | c[1]);
+		ll.hatype = (uint16_t)(((uint32_t)c[2] << 8) | c[3]);
+		ll.halen = (uint8_t)(((uint32_t)c[4] << 8) | c[5]);
+		memcpy(ll.addr, c + 6, 8);
+		memcpy(&ll.protocol, c + 14, 2);
+	}
+	*sll = ll;
+	p->pos += p->hdrsize + caplen;
+	return caplen;
+}
+
 // The replay loop: read -> [BPF filter on the device] -> device walk (pipelined,
 // `depth` batches in flight) -> host formatter -> [tprintf wrap] -> out_fd.
 // Writes the text dissector_entry_point prints for each accepted record, in
@@ -274,11 +331,14 @@ static bool write_all(int fd, const void *buf, size_t n)
 // (ctx->magic / ctx->link_type, netsniff-ng.c:694-695): the *_LL remap undone
 // (the stored magic), version 2.4, thiszone 0, sigfigs 0, snaplen 65535,
 // link type swapped once more when the magic is a swapped one (as the
-// reference does with the as-stored value)
+// reference does with the as-stored value).  A swapped SLL / netlink file
+// holds the remapped magic swab32(*_MAGIC_LL), which pcap_magic_is_swapped
+// does not recognise (pcap_io.h:307-320): its header is written unswapped,
+// the link type as stored.
 static bool push_fhdr(const nsd_pcap *p, int fd)
 {
 	uint8_t h[24];
-	const bool sw = p->swapped;
+	const bool sw = p->swapped && p->ll_extra == 0;
 	const uint16_t vmaj = sw ? bswap16(2) : 2, vmin = sw ? bswap16(4) : 4;
 	const uint32_t zero = 0, snap = sw ? bswap32(65535) : 65535;
 	const uint32_t lt = sw ? bswap32(p->linktype) : p->linktype;
@@ -314,7 +374,9 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		return NSD_ERR_ARG;
 	const int lt = (int)p->linktype;
 	const bool has_ll = p->ll_extra != 0;   // *_LL file: one sockaddr_ll per record
-	const uint32_t ext_words = 64 * BATCH;
+	// room for every record of the batch to take a deep (> 16 layer) entry;
+	// a chain the pool still cannot hold is re-rendered on the host (below)
+	const uint32_t ext_words = 2u * NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS) * BATCH;
 	if (pcap_fd >= 0 && !push_fhdr(p, pcap_fd)) {
 		nsd_pcap_close(p);
 		return NSD_ERR_ARG;
@@ -355,6 +417,26 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		    (pcap_fd >= 0 && !x.rhdr))
 			rc = NSD_ERR_NOMEM;
 	}
+	// text out (tprintf-wrapped at `cols` > 0), then the records to the pcap
+	// write-out, for `n` records whose text is in `text`
+	auto emit = [&](uint32_t n, const std::string &recs) -> long {
+		const char *w = text.data();
+		size_t wn = text.size();
+		if (cols > 0 && wn) {
+			wrapped.resize(2 * wn + 16);
+			long k = nsd_tprintf_wrap(text.data(), wn, cols, &wrap_state, &wrapped[0], wrapped.size());
+			if (k < 0)
+				return k;
+			w = wrapped.data();
+			wn = (size_t)k;
+		}
+		if (!write_all(out_fd, w, wn))
+			return NSD_ERR_ARG;
+		if (pcap_fd >= 0 && !write_all(pcap_fd, recs.data(), recs.size()))
+			return NSD_ERR_ARG;
+		printed += n;
+		return NSD_OK;
+	};
 	// complete the oldest batch and print it
 	auto finish = [&](Batch &x) -> long {
 		int st = nsd_pipe_wait(pipe);
@@ -371,21 +453,52 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		// join the pieces in order
 		const uint32_t nt = x.n < 2048 ? 1u : (uint32_t)threads;
 		std::vector<std::string> part(nt);
-		std::vector<long> prc(nt, 0);
+		std::vector<long> prc(nt, NSD_OK);
 		auto render = [&](uint32_t t) {
 			const uint32_t lo = (uint32_t)((uint64_t)x.n * t / nt), hi = (uint32_t)((uint64_t)x.n * (t + 1) / nt);
 			size_t cap = 256 * (size_t)(hi - lo) + 4096;
+			std::vector<uint64_t> ends(hi - lo);
+			std::vector<int8_t> st(hi - lo);
 			for (;;) {
 				part[t].resize(cap);
 				long r = nsd_format_batch_sll(x.frames, x.desc + lo, x.sll ? x.sll + lo : nullptr,
 							      hi - lo, lt, mode, x.rec + lo, x.ext, &part[t][0],
-							      cap, nullptr, nullptr);
+							      cap, ends.data(), st.data());
 				if (r >= 0) {
 					part[t].resize((size_t)r);
 					break;
 				}
 				cap = (size_t)(-r);
 			}
+			// a record that could not hold its chain (NSD_F_OVERFLOW: longer
+			// than NSD_EXT_MAX_LAYERS layers, or the ext pool was exhausted)
+			// is rendered by the per-packet path, which has no layer budget;
+			// any other status is an error
+			bool redo = false;
+			for (uint32_t k = lo; k < hi; k++) {
+				if (!st[k - lo])
+					continue;
+				if (!(x.rec[k].nflags & NSD_F_OVERFLOW)) {
+					prc[t] = NSD_ERR_FORMAT;
+					return;
+				}
+				redo = true;
+			}
+			if (!redo)
+				return;
+			std::string fixed;
+			size_t prev = 0;
+			for (uint32_t k = lo; k < hi; k++) {
+				const size_t e = (size_t)ends[k - lo];
+				if (st[k - lo])
+					nsd::render_packet_cpu(fixed, x.frames + NSD_DESC_OFF(x.desc[k]),
+							       NSD_DESC_CAPLEN(x.desc[k]), lt, mode,
+							       x.sll ? x.sll + k : nullptr);
+				else
+					fixed.append(part[t], prev, e - prev);
+				prev = e;
+			}
+			part[t].swap(fixed);
 		};
 		if (nt == 1) {
 			render(0);
@@ -397,46 +510,75 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			for (auto &h : th)
 				h.join();
 		}
+		for (long r : prc)
+			if (r != NSD_OK)
+				return r;
 		text.clear();
 		for (auto &q : part)
 			text += q;
-		const char *w = text.data();
-		size_t wn = text.size();
-		if (cols > 0 && wn) {
-			wrapped.resize(2 * wn + 16);
-			long k = nsd_tprintf_wrap(text.data(), wn, cols, &wrap_state, &wrapped[0], wrapped.size());
-			if (k < 0)
-				return k;
-			w = wrapped.data();
-			wn = (size_t)k;
-		}
-		while (wn) {
-			ssize_t r = write(out_fd, w, wn);
-			if (r < 0 && errno == EINTR)
-				continue;
-			if (r <= 0)
-				return NSD_ERR_ARG;
-			w += r;
-			wn -= (size_t)r;
-		}
-		if (pcap_fd >= 0) {
-			std::string rec_out;
+		std::string recs;
+		if (pcap_fd >= 0)
 			for (uint32_t k = 0; k < x.n; k++) {
-				rec_out.append((const char *)x.rhdr + 32 * (size_t)k, p->hdrsize);
-				rec_out.append((const char *)x.frames + NSD_DESC_OFF(x.desc[k]), NSD_DESC_CAPLEN(x.desc[k]));
+				recs.append((const char *)x.rhdr + 32 * (size_t)k, p->hdrsize);
+				recs.append((const char *)x.frames + NSD_DESC_OFF(x.desc[k]), NSD_DESC_CAPLEN(x.desc[k]));
 			}
-			if (!write_all(pcap_fd, rec_out.data(), rec_out.size()))
-				return NSD_ERR_ARG;
-		}
-		printed += x.n;
-		return NSD_OK;
+		return emit(x.n, recs);
 	};
+	// complete every batch in flight, in submission order
 	int slot = 0;
+	auto drain = [&]() -> long {
+		long r0 = NSD_OK;
+		for (int k = 0; k < DEPTH; k++) {
+			Batch &x = b[(slot + k) % DEPTH];
+			if (x.busy) {
+				long r = finish(x);
+				if (r0 == NSD_OK)
+					r0 = r;
+			}
+		}
+		return r0;
+	};
+	// a record longer than a batch can carry: after the batches before it,
+	// filtered and dissected on its own through the per-packet path
+	std::vector<uint8_t> big;
+	auto one_big = [&]() -> long {
+		long r = drain();
+		if (r != NSD_OK)
+			return r;
+		nsd_sll_t ll;
+		uint8_t hdr[32];
+		const long caplen = read_one(p, big, &ll, hdr);
+		if (caplen <= 0)
+			return NSD_OK;
+		if (filter) {
+			const nsd_desc_t d = NSD_DESC(0, caplen);
+			uint32_t v = 0;
+			r = nsd_bpf_filter_batch(filter, big.data(), (size_t)caplen, &d, 1, &v);
+			if (r != NSD_OK)
+				return r;
+			if (!v)
+				return NSD_OK;
+		}
+		if (counters)
+			nsd::cpu_count_packet(big.data(), (uint32_t)caplen, lt, mode, has_ll ? &ll : nullptr, counters);
+		text.clear();
+		nsd::render_packet_cpu(text, big.data(), (size_t)caplen, lt, mode, has_ll ? &ll : nullptr);
+		std::string recs;
+		if (pcap_fd >= 0) {
+			recs.append((const char *)hdr, p->hdrsize);
+			recs.append((const char *)big.data(), (size_t)caplen);
+		}
+		return emit(1, recs);
+	};
 	while (rc == NSD_OK) {
 		Batch &x = b[slot];
 		if (x.busy && (rc = finish(x)) != NSD_OK)
 			break;
 		long n = read_batch(p, x.frames, FRAME_BYTES, x.desc, x.sll, BATCH, nullptr, nullptr, x.rhdr);
+		if (n == NSD_ERR_CAPLEN) {
+			rc = one_big();
+			continue;
+		}
 		if (n < 0) {
 			rc = n;
 			break;
@@ -479,14 +621,10 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		x.busy = true;
 		slot = (slot + 1) % DEPTH;
 	}
-	// drain in submission order
-	for (int k = 0; k < DEPTH; k++) {
-		Batch &x = b[(slot + k) % DEPTH];
-		if (x.busy) {
-			long r = finish(x);
-			if (rc == NSD_OK)
-				rc = r;
-		}
+	{
+		const long r = drain();
+		if (rc == NSD_OK)
+			rc = r;
 	}
 	for (auto &x : b) {
 		nsd_host_free(x.frames);

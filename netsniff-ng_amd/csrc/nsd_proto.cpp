@@ -44,6 +44,8 @@ void render_hex(std::string &s, const uint8_t *pkt, uint32_t caplen, uint32_t fr
 void render_ascii(std::string &s, const uint8_t *pkt, uint32_t caplen, uint32_t from, uint32_t len);
 int cpu_step(int mode, const uint8_t *pkt, uint32_t caplen, int id, uint32_t &data, uint32_t &tail,
 	     uint16_t &ip_csum, uint8_t &flags, const nsd_sll_t *sll);
+void render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
+		       const nsd_sll_t *sll);
 }
 
 extern "C" __attribute__((visibility("hidden"))) void nsd_device_ctx_release(void);
@@ -63,6 +65,7 @@ namespace {
 
 std::string g_out;          // text of the current packet when there is no tprintf
 long g_line_count = 0;      // __tprintf_flush's line counter for that case
+thread_local std::string *t_capture = nullptr;   // render_packet_cpu's sink
 
 int tty_cols()
 {
@@ -76,6 +79,10 @@ void out(const char *p, size_t n)
 {
 	if (!n)
 		return;
+	if (t_capture) {
+		t_capture->append(p, n);
+		return;
+	}
 	if (tprintf) {
 		for (size_t i = 0; i < n; i += 256) {
 			const size_t k = n - i < 256 ? n - i : 256;
@@ -319,6 +326,34 @@ struct protocol *ops_of(int id)
 
 bool is_lt(int lt, uint32_t v) { return (uint32_t)lt == v || (uint32_t)lt == __builtin_bswap32(v); }
 
+// the ops id of one of this library's ops objects, 0 for others
+int id_of(const struct protocol *p)
+{
+	for (int id = 1; id < NSD_OPS_COUNT; id++)
+		if (id != NSD_OPS_NLMSG && id != NSD_OPS_IEEE80211 && ops_of(id) == p)
+			return id;
+	return 0;
+}
+
+// start / exit ops per link type (dissector.c:75-104; byte-swapped link
+// types match too, :79)
+void start_end(int linktype, struct protocol *&start, struct protocol *&end)
+{
+	end = &none_ops;
+	if (is_lt(linktype, NSD_LINKTYPE_EN10MB)) {
+		start = &ethernet_ops;
+	} else if (is_lt(linktype, NSD_LINKTYPE_IEEE802_11_RADIOTAP) || is_lt(linktype, NSD_LINKTYPE_IEEE802_11)) {
+		start = &ieee80211_ops;
+	} else if (is_lt(linktype, NSD_LINKTYPE_NETLINK)) {
+		start = &nlmsg_ops;
+	} else if (is_lt(linktype, NSD_LINKTYPE_LINUX_SLL)) {
+		start = &sll_ops;
+	} else {
+		start = &none_ops;
+		end = nullptr;
+	}
+}
+
 std::string g_etcdir = NSD_ETCDIRE;
 
 } // namespace
@@ -406,22 +441,7 @@ extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype,
 	t_frame.caplen = (uint32_t)len;
 
 	struct protocol *start, *end;
-	if (is_lt(linktype, NSD_LINKTYPE_EN10MB)) {
-		start = &ethernet_ops;
-		end = &none_ops;
-	} else if (is_lt(linktype, NSD_LINKTYPE_IEEE802_11_RADIOTAP) || is_lt(linktype, NSD_LINKTYPE_IEEE802_11)) {
-		start = &ieee80211_ops;
-		end = &none_ops;
-	} else if (is_lt(linktype, NSD_LINKTYPE_NETLINK)) {
-		start = &nlmsg_ops;
-		end = &none_ops;
-	} else if (is_lt(linktype, NSD_LINKTYPE_LINUX_SLL)) {
-		start = &sll_ops;
-		end = &none_ops;
-	} else {
-		start = &none_ops;
-		end = nullptr;
-	}
+	start_end(linktype, start, end);
 	dissector_main(&pkt, start, end);
 
 	switch (mode) {
@@ -431,4 +451,55 @@ extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype,
 	}
 	flush();
 	t_frame.head = nullptr;
+}
+
+// One packet's text as dissector_entry_point prints it when every ops object
+// is set to `mode` (dissector_init_all(mode) + dissector_entry_point(...,
+// mode, ...), as read_pcap calls them), appended to out instead of going to
+// tprintf.  The pcap replay uses it for the records a batch cannot carry: a
+// frame above NSD_MAX_CAPLEN, or a chain the record and its ext pool could
+// not hold (NSD_F_OVERFLOW).  The reference objects' 802.11 / netlink ops
+// run with whatever print type their initialiser gave them.
+void nsd::render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
+			    const nsd_sll_t *sll)
+{
+	if (mode == PRINT_NONE)
+		return;
+	struct sockaddr_ll *ll = (struct sockaddr_ll *)sll;
+	struct pkt_buff pkt;
+	pkt.head = (uint8_t *)packet;
+	pkt.data = (uint8_t *)packet;
+	pkt.tail = (uint8_t *)packet + len;
+	pkt.dissector = nullptr;
+	pkt.link_type = (uint32_t)linktype;
+	pkt.sll = ll;
+	const FrameCtx saved = t_frame;
+	std::string *const saved_cap = t_capture;
+	t_frame.head = packet;
+	t_frame.caplen = (uint32_t)len;
+	t_capture = &text;
+	struct protocol *start, *end;
+	start_end(linktype, start, end);
+	if (mode == PRINT_NORM || mode == PRINT_LESS) {
+		for (pkt.dissector = start; pkt.dissector;) {
+			struct protocol *d = pkt.dissector;
+			pkt.dissector = nullptr;
+			const int id = id_of(d);
+			if (id)
+				run_layer(&pkt, id, mode);
+			else if (d->process)
+				d->process(&pkt);
+			else
+				break;
+		}
+		if (end == &none_ops)
+			(mode == PRINT_NORM ? hex_ascii_impl : none_less)(&pkt);
+	}
+	switch (mode) {
+	case PRINT_HEX: hex_impl(&pkt); break;
+	case PRINT_ASCII: ascii_impl(&pkt); break;
+	case PRINT_HEX_ASCII: hex_ascii_impl(&pkt); break;
+	}
+	t_capture = saved_cap;
+	t_frame = saved;
 }

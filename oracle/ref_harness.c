@@ -296,16 +296,17 @@ int main(int argc, char **argv)
 	swap = fh[0] == 0xd4c3b2a1u || fh[0] == 0x4d3cb2a1u;
 	if (index_out)
 		fi = fopen(index_out, "wb");
-	buf = calloc(1, 65536 + 4096);
+	/* read_pcap's reused 1 MiB `out` buffer (netsniff-ng.c:680-681) */
+	buf = calloc(1, (1 << 20) + 4096);
 	for (;;) {
 		uint32_t rh[4], caplen;
 		uint64_t pos;
 		if (fread(rh, 4, 4, f) != 4)
 			break;
 		caplen = sw32(rh[2], swap);
-		if (caplen > 65536)
+		if (caplen > (1 << 20))
 			return 1;
-		memset(buf, 0, 65536 + 4096);
+		memset(buf, 0, caplen + 4096);
 		if (fread(buf, 1, caplen, f) != caplen)
 			break;
 		g_caplen = caplen;

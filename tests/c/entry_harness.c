@@ -9,11 +9,11 @@
  *   dissector_cleanup_all()                       netsniff-ng.c:764
  *
  * The executable provides tprintf / tprintf_flush (as netsniff-ng's
- * tprintf.o does); this one appends the text unwrapped to a buffer, and the
- * per-packet text ends are written beside it, so tests compare them with the
- * golden per-packet text.  Test infrastructure.
+ * tprintf.o does: the same 1 KiB buffer and wrap rules, into memory instead
+ * of stdout), and the per-packet text ends are written beside it, so tests
+ * compare them with the golden per-packet text.  Test infrastructure.
  *
- *   entry_harness -m MODE [-e ETCDIR] [-r REPS] in.pcap out.txt out.ends
+ *   entry_harness -m MODE [-e ETCDIR] [-w COLS] [-r REPS] in.pcap out.txt out.ends
  *   -r REPS: timing mode (text discarded after every packet, the loop over
  *   all records repeated REPS times; prints "pkts=N us_per_pkt=X" on stdout)
  */
@@ -27,32 +27,81 @@
 
 #include "../../include/netsniff_dissect.h"
 
+/* netsniff-ng's tprintf (tprintf.c:65-162), restated: a 1 KiB buffer,
+ * flushed when a piece does not fit and by tprintf_flush, each flush wrapped
+ * for a terminal `g_cols` wide (-w, default 65535 like nsref -w 65535); the
+ * flushed text goes to tbuf */
 static char *tbuf;
 static size_t tlen, tcap;
+static char buffer[1024];
+static size_t buffer_use;
+static int g_cols = 65535;
+static long line_count;
 
-void tprintf(char *msg, ...)
+static void put(char c)
 {
-	va_list vl;
-	char tmp[4096];
-	va_start(vl, msg);
-	int n = vsnprintf(tmp, sizeof(tmp), msg, vl);
-	va_end(vl);
-	if (n < 0)
-		abort();
-	if ((size_t)n >= sizeof(tmp))
-		abort();   /* the reference panics past its 1 KiB buffer */
-	if (tlen + (size_t)n > tcap) {
-		tcap = (tlen + n) * 2 + 4096;
+	if (tlen + 1 > tcap) {
+		tcap = tcap * 2 + 65536;
 		tbuf = realloc(tbuf, tcap);
 		if (!tbuf)
 			abort();
 	}
-	memcpy(tbuf + tlen, tmp, n);
-	tlen += n;
+	tbuf[tlen++] = c;
+}
+
+static void flush_buffer(void)
+{
+	long term_len = g_cols - 5;
+	size_t color_open = 0;
+	for (size_t i = 0; i < buffer_use; ++i) {
+		if (buffer[i] == '\n') {
+			term_len = g_cols - 5;
+			line_count = -1;
+		}
+		if (buffer[i] == 033 && i + 1 < buffer_use && buffer[i + 1] == '[')
+			color_open++;
+		if (color_open == 0 && line_count >= term_len) {
+			put('\n');
+			for (int k = 0; k < 3; k++)
+				put(' ');
+			line_count = 3;
+			while (i < buffer_use && (buffer[i] == ' ' || buffer[i] == ','))
+				i++;
+		}
+		if (color_open > 0 && buffer[i] == 'm')
+			color_open--;
+		put(buffer[i]);
+		line_count++;
+	}
+	buffer_use = 0;
+}
+
+void tprintf(char *msg, ...)
+{
+	va_list vl;
+	size_t avail = sizeof(buffer) - buffer_use;
+	va_start(vl, msg);
+	int ret = vsnprintf(buffer + buffer_use, avail, msg, vl);
+	va_end(vl);
+	if (ret < 0 || (size_t)ret > sizeof(buffer))
+		abort();   /* the reference panics */
+	if ((size_t)ret >= avail) {
+		flush_buffer();
+		va_start(vl, msg);
+		ret = vsnprintf(buffer, sizeof(buffer), msg, vl);
+		va_end(vl);
+		if (ret < 0)
+			abort();
+	}
+	buffer_use += ret;
 }
 
 static size_t flushes;
-void tprintf_flush(void) { flushes++; }
+void tprintf_flush(void)
+{
+	flushes++;
+	flush_buffer();
+}
 
 static uint32_t sw32(uint32_t v, int s) { return s ? __builtin_bswap32(v) : v; }
 
@@ -60,8 +109,9 @@ int main(int argc, char **argv)
 {
 	int mode = PRINT_NORM, reps = 0, c;
 	const char *etc = "/nonexistent-netsniff-ng-etc";
-	while ((c = getopt(argc, argv, "m:e:r:")) != -1) {
+	while ((c = getopt(argc, argv, "m:e:r:w:")) != -1) {
 		if (c == 'm') mode = atoi(optarg);
+		else if (c == 'w') g_cols = atoi(optarg);
 		else if (c == 'e') etc = optarg;
 		else if (c == 'r') reps = atoi(optarg);
 		else return 2;
@@ -118,7 +168,7 @@ int main(int argc, char **argv)
 			for (size_t i = 0; i < nrec; i++) {
 				memcpy(buf, file + offs[i], caps[i]);
 				dissector_entry_point(buf, caps[i], (int)linktype, mode, (struct sockaddr_ll *)&sll);
-				tlen = 0;
+				tlen = 0;   /* the text is written nowhere (/dev/null) */
 			}
 		}
 		clock_gettime(CLOCK_MONOTONIC, &t1);

@@ -3,6 +3,8 @@
 
   tiny.pcap            C1: 1000 x 64 B Eth/IPv4/UDP
   edge.pcap            tests/edge_cases.py (every §8a quirk)
+  big.pcap             records longer than a batch carries (NSD_MAX_CAPLEN <
+                       caplen <= read_pcap's 1 MiB buffer) between short ones
   <pcap>.m<M>.w<C>.txt.gz / .ends.json
                        text printed by the REFERENCE parser objects
                        (oracle/_ref/nsref) for print mode M, terminal width C
@@ -65,8 +67,46 @@ def rec_digest(rec, ext):
     return h.hexdigest()
 
 
+def big_cases():
+    """Frames above 65535 bytes (tcpdump's default snaplen is 262144; GRO
+    frames), with payload patterns that compress: Eth/IPv4/UDP (tot_len at
+    its u16 maximum: the IPv4 trim cuts the tail), Eth/IPv4/ICMP echo (the
+    checksum reads the whole post-trim message), Eth/IPv6/HBH/UDP, between
+    short frames of tiny.pcap and edge.pcap."""
+    import struct
+    lt, tiny = T.read_pcap(os.path.join(HERE, "tiny.pcap"))
+    _, edge = T.read_pcap(os.path.join(HERE, "edge.pcap"))
+
+    def pay(n, k):
+        return bytes((i * k) % 251 for i in range(n))
+
+    eth4 = bytes.fromhex("0a0b0c0d0e0f" "020304050607" "0800")
+    eth6 = bytes.fromhex("0a0b0c0d0e0f" "020304050607" "86dd")
+
+    def ipv4(proto, tot_len):
+        h = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0, tot_len, 7, 0x4000, 64, proto, 0,
+                                  bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2])))
+        s = sum(struct.unpack(">10H", bytes(h)))
+        s = (s & 0xFFFF) + (s >> 16)
+        s = (s & 0xFFFF) + (s >> 16)
+        h[10:12] = struct.pack(">H", ~s & 0xFFFF)
+        return bytes(h)
+
+    udp_big = eth4 + ipv4(17, 65535) + struct.pack(">HHHH", 5353, 53, 65515, 0) + pay(70000 - 42, 7)
+    icmp_big = eth4 + ipv4(1, 65535) + bytes([8, 0, 0x12, 0x34, 0, 1, 0, 2]) + pay(66002 - 42, 13)
+    v6 = (eth6 + bytes([0x60, 0, 0, 0]) + struct.pack(">HBB", 0, 0, 64) + bytes(range(32))
+          + bytes([17, 0, 1, 4, 0, 0, 0, 0]) + struct.pack(">HHHH", 1000, 2000, 8, 0) + pay(100000 - 70, 3))
+    return [tiny[0], udp_big, edge[5], icmp_big, v6, tiny[1]]
+
+
 def main():
     T.build_native()
+    big = os.path.join(HERE, "big.pcap")
+    T.write_pcap(big, big_cases())
+    for m in MODES:
+        save_text(os.path.join(HERE, f"big.m{m}.w65535"), T.run_ref(big, mode=m, cols=65535))
+    if "--big-only" in sys.argv:
+        return
     tiny = os.path.join(HERE, "tiny.pcap")
     edge = os.path.join(HERE, "edge.pcap")
     T.synth().nsd_synth_pcap(T.SYN_UDP64, T.SEED, 0, 1000, tiny.encode())

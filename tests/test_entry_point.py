@@ -34,9 +34,9 @@ def harness(tmp_path_factory):
     return exe
 
 
-def run_harness(exe, pcap, mode, tmp_path, etc=None):
+def run_harness(exe, pcap, mode, tmp_path, etc=None, cols=65535):
     txt, ends = str(tmp_path / f"m{mode}.txt"), str(tmp_path / f"m{mode}.ends")
-    args = [exe, "-m", str(mode)] + (["-e", etc] if etc else []) + [pcap, txt, ends]
+    args = [exe, "-m", str(mode), "-w", str(cols)] + (["-e", etc] if etc else []) + [pcap, txt, ends]
     r = subprocess.run(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
     assert r.returncode == 0, f"harness rc={r.returncode}: {r.stderr[-2000:]!r}"
     with open(txt, "rb") as f:
@@ -48,7 +48,7 @@ def run_harness(exe, pcap, mode, tmp_path, etc=None):
     return out, r.stderr
 
 
-@pytest.mark.parametrize("name", ["tiny", "edge"])
+@pytest.mark.parametrize("name", ["tiny", "edge", "big"])
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX, T.PRINT_ASCII, T.PRINT_HEX_ASCII])
 def test_entry_point_matches_golden(harness, tmp_path, name, mode):
     gold = load_golden(f"{name}.m{mode}.w65535")
@@ -58,6 +58,17 @@ def test_entry_point_matches_golden(harness, tmp_path, name, mode):
     assert not bad, f"packets {bad[:10]} differ; first: {got[bad[0]][:300]!r} vs {gold[bad[0]][:300]!r}"
     # no conf dir: lookup_init's message for each of the four tables (lookup.c:48-51)
     assert err.count(b"Port name resolution won't be available.") == 4
+
+
+@pytest.mark.parametrize("name", ["tiny", "edge"])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_entry_point_wrapped_80(harness, tmp_path, name, mode):
+    """Through netsniff-ng's tprintf at 80 columns (the harness restates
+    tprintf.c's buffer and wrap) == the reference objects' wrapped text."""
+    gold = load_golden(f"{name}.m{mode}.w80")
+    got, _ = run_harness(harness, os.path.join(T.GOLDEN, name + ".pcap"), mode, tmp_path, cols=80)
+    bad = [i for i in range(len(gold)) if got[i] != gold[i]]
+    assert not bad, f"packets {bad[:10]} differ; first: {got[bad[0]][:300]!r} vs {gold[bad[0]][:300]!r}"
 
 
 def test_entry_point_print_none(harness, tmp_path):
