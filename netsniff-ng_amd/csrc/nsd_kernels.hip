@@ -16,12 +16,12 @@
 // Each lane's window is one LDS row of 17 dwords (an odd stride): 64 lanes
 // reading the same header offset hit 64 different banks.
 //
-// Pass 1 (dissect_fast) finishes every packet whose chain resolves inside its
-// first 64 bytes, with the next tile's chunks and the tile after next's
-// descriptors in flight while the current tile is walked from LDS only.  The
-// rest is compacted into a queue (ballot + one atomic per wave + mbcnt) for
-// pass 2 (dissect_general): per-lane window restaging at each lane's cursor,
-// ext spill, per-lane ICMPv4 payload checksums.
+// The fast walk finishes every packet whose chain resolves inside its first
+// 64 bytes, with the next tile's chunks and the tile after next's descriptors
+// in flight while the current tile is walked from LDS only.  The tile's
+// other lanes continue at once with the general walk (continue_walk):
+// per-lane window restaging at each lane's cursor, ext spill; ICMPv4 payload
+// checksums longer than a window are summed by the block at the end.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,7 +35,7 @@ constexpr int WIN1 = 64;         // bytes per staged window, pass 1
 #ifndef NSD_WIN2
 #define NSD_WIN2 64
 #endif
-constexpr int WIN2 = NSD_WIN2;   // bytes per staged window, pass 2
+constexpr int WIN2 = NSD_WIN2;   // bytes per staged window, general-walk continuation
 // window row stride in dwords (odd: 64 lanes reading the same offset hit 64
 // different banks)
 constexpr int row_of(int W) { return W / 4 + 1; }
@@ -44,12 +44,6 @@ constexpr int row_of(int W) { return W / 4 + 1; }
 #endif
 #ifndef NSD_MINW
 #define NSD_MINW 4                 // waves per SIMD the fused kernel is register-allocated for
-#endif
-#ifndef NSD_P1_TILES
-#define NSD_P1_TILES 16            // pass-1 grid strides per pass-2 round (0: whole shard)
-#endif
-#ifndef NSD_P2_WAVES
-#define NSD_P2_WAVES 4             // waves of a block that walk its pass-2 queue
 #endif
 #ifndef NSD_CSUM_SPLIT
 #define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
@@ -362,10 +356,8 @@ __device__ __forceinline__ void block_flush(unsigned long long *s_cnt, unsigned 
 }
 
 // Pending ICMPv4 checksums: entry = packet index | message offset << 32 |
-// message length << 48 (offsets and lengths are < 65536).  Block b keeps
-// PLISTS lists: one per pass-1 wave, then pass 2's.
-constexpr int PLISTS = WAVES + 1;
-
+// message length << 48 (offsets and lengths are < 65536).  Each wave of a
+// block keeps one list (room for every packet it visits).
 __device__ __forceinline__ uint64_t pend_entry(uint32_t i, uint32_t off, uint32_t len)
 {
 	return (uint64_t)i | (uint64_t)(off & 0xFFFF) << 32 | (uint64_t)(len & 0xFFFF) << 48;
@@ -375,47 +367,171 @@ __device__ __forceinline__ uint64_t pend_entry(uint32_t i, uint32_t off, uint32_
 // Block-level shared state of one dissect launch.
 constexpr int WINMAX = WIN1 > WIN2 ? WIN1 : WIN2;
 struct Shared {
-	uint32_t win[WAVES][64 * row_of(WINMAX)];   // staged windows (pass 1, then pass 2)
+	uint32_t win[WAVES][64 * row_of(WINMAX)];   // staged windows (fast walk, then continuations)
 	unsigned long long cnt[NSD_NCOUNTERS];      // block counters
 	uint8_t lay3[256];                          // eth_lay3
 	uint32_t step[64];                          // c_step, c_lay2h (general walk)
-	uint32_t qn;                                // pass-1 deferrals queued
-	uint32_t pn;                                // pass-2 pending checksums
 	uint32_t wc[WAVES][2];                      // per-wave ext pool chunk {next word, words left}
-	uint32_t pcnt[WAVES];                       // pass-1 pending checksums per wave
-	uint32_t q2;                                // pass-2 queue entries taken
-	uint32_t lay[WAVES][NSD_LDS_LAYERS * 64];   // pass-2 layer lists (layers 6..15)
+	uint32_t pcnt[WAVES];                       // pending checksums per wave
+	uint32_t lay[WAVES][NSD_LDS_LAYERS * 64];   // general-walk layer lists (layers 6..15)
 };
 
-// ---- pass 1 ------------------------------------------------------------------
-// Every packet of the block's grid-stride tiles; packets whose chain does
-// not resolve inside their first 64 bytes are appended to the block's queue
-// (s_qn entries), ICMPv4 messages past the window to the wave's pending list
-// (s_pcnt[wave] entries).
+// The LINKTYPE_LINUX_SLL head (dissector_sll.c:39-82): pulls nothing; in
+// print_full the next ops come from the packet's sockaddr_ll (sll_next).
 template <int MODE>
-__device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ frames,
-				      const uint64_t *__restrict__ desc, uint32_t n, int start_id,
-				      uint4 *__restrict__ rec, uint4 *__restrict__ queue, uint32_t region,
-				      uint64_t *__restrict__ pend, uint32_t first, uint32_t end, uint32_t &npend)
+__device__ __forceinline__ void sll_head(Shared &sh, WalkOut &w, const uint32_t *__restrict__ sll, uint32_t i)
+{
+	const uint32_t w0 = sll ? sll[5 * (size_t)i] : 0u;       // sll_family | sll_protocol << 16
+	const uint32_t w2 = sll ? sll[5 * (size_t)i + 2] : 0u;   // sll_hatype | pkttype << 16 | halen << 24
+	const uint32_t hatype = w2 & 0xFFFF;
+	const uint32_t proto = __builtin_bswap16((uint16_t)(w0 >> 16));
+	w.chain = NSD_OPS_SLL;
+	w.n = 1;
+	atomicAdd(&sh.cnt[NSD_CNT_OPS + NSD_OPS_SLL], 1ull);
+	w.id = sll_next(hatype, proto, MODE, sh.step[32 + NSD_L2H(proto)]);
+}
+
+// What a lane whose general walk ended leaves behind (wave-uniform call):
+// an ICMPv4 message past its windows goes to the wave's pending list, an ext
+// chain to the pool (layers 0..5 from the record registers, 6..15 from the
+// wave's LDS list, deeper ones already in the entry), then the record and the
+// flag counts.
+template <int MODE>
+__device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, uint32_t caplen, const GenSink &g,
+					     uint4 *__restrict__ rec, uint64_t *__restrict__ wq, uint32_t &npend,
+					     FlagCnt &fc, int lane)
+{
+	if (MODE == PRINT_NORM) {
+		const bool pnd = fin && w.icmp_pend;
+		const uint64_t pm = __ballot(pnd);
+		if (pnd)
+			wq[npend + lanes_below(pm)] = pend_entry(i, w.icmp_off, w.icmp_len);
+		npend += (uint32_t)__popcll(pm);
+	}
+	const bool ex = fin && w.need_ext;
+	if (__ballot(ex)) {
+		const bool tk = ex && !w.ext_on;
+		const uint32_t sb = ext_take(g, tk, NSD_EXT_WORDS(NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS));
+		if (tk) {
+			w.slot = sb;
+			w.ext_on = true;
+		}
+		if (ex && w.slot == 0xFFFFFFFFu)
+			w.flags |= NSD_F_OVERFLOW;   // the pool is full
+		if (ex && w.slot != 0xFFFFFFFFu) {
+			uint32_t *e = g.pool + w.slot;
+			const uint32_t nl = w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS;
+			auto lv = [&](uint32_t j) -> uint32_t {
+				if (j < NSD_REC_MAX_LAYERS)
+					return ((w.chain >> (5 * j)) & 31) | (uint32_t)off_of(w, j) << 16;
+				return j < nl ? g.lay[(j - NSD_REC_MAX_LAYERS) * 64 + lane] : 0u;
+			};
+			*(uint4 *)e = make_uint4(i, nl, 0, 0);
+			*(uint4 *)(e + 4) = make_uint4(lv(0), lv(1), lv(2), lv(3));
+			if (nl > 4)
+				*(uint4 *)(e + 8) = make_uint4(lv(4), lv(5), lv(6), lv(7));
+			if (nl > 8)
+				*(uint4 *)(e + 12) = make_uint4(lv(8), lv(9), lv(10), lv(11));
+			if (nl > 12)
+				*(uint4 *)(e + 16) = make_uint4(lv(12), lv(13), lv(14), lv(15));
+		}
+	}
+	if (fin)
+		store_rec(rec, i, pack_record(w));
+	fc.add(w, caplen, fin);
+}
+
+// The lanes of a tile the fast walk could not finish inside their first 64
+// bytes, walked on at once by the general walk (gen_step): from where the
+// fast walk stopped (FW_RESUME: Ethernet, tags and the IP header recorded)
+// or from the start (FW_RESTART: other link types, MPLS, deeper tag stacks,
+// bytes past the first window).  A round stages each such lane's WIN2-byte
+// window at its cursor - the lines the fast walk has just read are still in
+// L2, the next ones are read once, 4 consecutive lanes per 64 bytes of a
+// window (coalesced) - and runs layers until the lane's chain ends or needs
+// bytes past the window; the wave repeats rounds until all its lanes are
+// done.  Measured alternatives (C4): a separate pass over queued
+// packets (the lines were evicted by then), per-step loads straight from
+// L2 (64 lines per wave instruction: the vector-memory address path, not the
+// bytes, bound it).
+template <int MODE>
+__device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restrict__ frames, uint64_t d,
+					      uint32_t i, uint32_t fw, WalkOut &w, int start_id,
+					      const uint32_t *__restrict__ sll, uint4 *__restrict__ rec,
+					      const GenSink &g, uint64_t *__restrict__ wq, uint32_t &npend, FlagCnt &fc)
+{
+	constexpr int ROW = row_of(WIN2);
+	const int lane = threadIdx.x & 63;
+	const int wv = threadIdx.x >> 6;
+	const bool on = fw != FW_DONE;
+	const uint32_t caplen = NSD_DESC_CAPLEN(d), m = (uint32_t)NSD_DESC_OFF(d) & 15;
+	if (on) {
+		if (fw == FW_RESTART) {
+			walk_init(w, caplen, start_id);
+			if (start_id == NSD_OPS_SLL)
+				sll_head<MODE>(sh, w, sll, i);
+		} else {
+			// the layers the fast walk ran (its finished chains are counted
+			// by chain word; these are counted here)
+			for (uint32_t k = 0; k < w.n; k++)
+				atomicAdd(&sh.cnt[NSD_CNT_OPS + ((w.chain >> (5 * k)) & 31)], 1ull);
+		}
+	}
+	bool have = on;
+	uint32_t wb = (w.data + m) & ~15u;
+	while (__ballot(have)) {
+		Chunks<WIN2> cc;
+		stage_load<true, WIN2>(cc, frames, d, wb | (have ? 0u : 0x80000000u), lane);
+		stage_write(&sh.win[wv][0], cc, lane);
+		wave_sync_lds();
+		const LSrc<false, WIN2> src{ &sh.win[wv][lane * ROW], sh.lay3, sh.step, frames + NSD_DESC_OFF(d),
+					     caplen, m, wb, false };
+		bool susp;
+		for (;;) {
+			const bool run = have && w.id != 0;
+			susp = run && src.near_end(w.data, w.id);
+			const bool act = run && !susp;
+			if (!__ballot(act))
+				break;
+			gen_step<MODE>(src, act, w, g);
+		}
+		wave_sync_lds();
+		emit_general<MODE>(have && !susp, w, i, caplen, g, rec, wq, npend, fc, lane);
+		have = have && susp;
+		if (susp)
+			wb = (w.data + m) & ~15u;
+	}
+}
+
+// ---- the walk ------------------------------------------------------------------
+// Every packet of the block's grid-stride tiles, one wave per 64-packet tile:
+// the fast walk over each packet's first 64 bytes, then the general walk
+// for the lanes it could not finish (continue_walk); ICMPv4 messages past
+// the windows go to the wave's pending list (npend entries).
+template <int MODE>
+__device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict__ frames,
+					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
+					   uint4 *__restrict__ rec, uint64_t *__restrict__ pend, uint32_t region,
+					   uint32_t *__restrict__ ext, uint32_t ext_words, uint32_t *__restrict__ ext_used,
+					   uint32_t chunk, const uint32_t *__restrict__ sll, uint32_t &npend)
 {
 	constexpr int ROW = row_of(WIN1);
 	auto &s_win = sh.win;
-	auto &s_qn = sh.qn;
 	unsigned long long *const s_cnt = sh.cnt;
 	const uint8_t *const s_lay3 = sh.lay3;
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
 
 	const uint32_t stride = gridDim.x * BLOCK;
-	uint4 *const bq = queue + (size_t)blockIdx.x * region;   // this block's queue region
 	// this wave's pending-checksum list (a wave visits region / WAVES packets)
 	uint64_t *const wq = pend + ((size_t)blockIdx.x * WAVES + wv) * (region / WAVES);
+	const GenSink g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, &sh.lay[wv][0] };
 	FlagCnt fc;
-	uint32_t base = first + blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
+	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
 
 	if (MODE != PRINT_NORM && MODE != PRINT_LESS) {
 		// every process() is NULL: no chain (dissector.c:51-53)
-		for (; base < end; base += stride) {
+		for (; base < n; base += stride) {
 			const uint32_t i = base + lane;
 			fc.pkts += FlagCnt::pc(i < n);
 			if (i < n) {
@@ -430,14 +546,14 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 
 	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
 	// descriptors are in flight
-	if (base >= end)
+	if (base >= n)
 		return;
 	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
-	uint64_t d1 = (base + stride < end && base + stride + lane < n) ? desc[base + stride + lane] : 0;
+	uint64_t d1 = (base + stride < n && base + stride + lane < n) ? desc[base + stride + lane] : 0;
 	Chunks<WIN1> ch;
 	stage_load<false, WIN1>(ch, frames, d0, 0, lane);
 
-	for (; base < end; base += stride) {
+	for (; base < n; base += stride) {
 		const uint32_t i = base + lane;
 		const bool valid = i < n;
 		const uint64_t off = NSD_DESC_OFF(d0);
@@ -446,9 +562,9 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 		stage_write(&s_win[wv][0], ch, lane);
 		// prefetch: descriptors of tile t+2, chunks of tile t+1
 		const uint32_t b2 = base + 2 * stride;
-		const uint64_t d2 = (b2 < end && b2 + lane < n) ? desc[b2 + lane] : 0;
+		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
 		const uint32_t b1 = base + stride;
-		if (b1 < end)
+		if (b1 < n)
 			stage_load<false, WIN1>(ch, frames, d1, 0, lane);
 		wave_sync_lds();
 
@@ -457,49 +573,30 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 		uint32_t fw = FW_DONE;
 		if (valid) {
 			const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
-					      (uint32_t)off & 15, 0, false };
+						    (uint32_t)off & 15, 0, false };
 			fw = fast_walk<MODE>(src, caplen, w);
 		}
 		const bool deferred = fw != FW_DONE;
 		wave_sync_lds();
+		const bool done = valid && !deferred;
 		if (MODE == PRINT_NORM) {
 			// ICMPv4 messages past the window: listed for the checksum pass, which
 			// patches the record if the sum is bad
-			const bool pnd = w.icmp_pend && !deferred;
+			const bool pnd = w.icmp_pend && done;
 			const uint64_t pmask = __ballot(pnd);
 			if (pnd)
 				wq[npend + lanes_below(pmask)] = pend_entry(i, w.icmp_off, w.icmp_len);
 			npend += (uint32_t)__popcll(pmask);
 		}
-
-		const uint64_t dm = __ballot(deferred);
-		if (dm) {
-			const int leader = __ffsll((unsigned long long)dm) - 1;
-			uint32_t qb = 0;
-			if (lane == leader)
-				qb = atomicAdd(&s_qn, (uint32_t)__popcll(dm));   // LDS: no global contention
-			qb = __shfl(qb, leader, 64);
-			// queue entry: the packet, and where pass 2 resumes its walk
-			// (cursor, tail, layers so far, next ops, IPv4 checksum) or 0
-			// for a walk from the start
-			if (deferred)
-				bq[qb + lanes_below(dm)] =
-					fw == FW_RESUME
-						? make_uint4(i, w.data | w.tail << 16,
-							     (w.chain & 0xFFFFF) | (uint32_t)w.id << 20 | w.n << 25 | 1u << 31,
-							     w.ip_csum)
-						: make_uint4(i, 0, 0, 0);
-		}
-		const bool done = valid && !deferred;
 		// per-ops counts from the finished chains, grouped by chain word
 		// (ids are >= 1, so equal chain words imply equal layer counts)
 		{
 			uint32_t key = done ? w.chain : 0xFFFFFFFFu;
 			for (;;) {
-				const uint64_t pend = __ballot(key != 0xFFFFFFFFu);
-				if (!pend)
+				const uint64_t pm = __ballot(key != 0xFFFFFFFFu);
+				if (!pm)
 					break;
-				const int leader = __ffsll((unsigned long long)pend) - 1;
+				const int leader = __ffsll((unsigned long long)pm) - 1;
 				const uint32_t lk = __shfl(key, leader, 64);
 				const uint64_t m = __ballot(key == lk);
 				if (lane == leader) {
@@ -515,201 +612,12 @@ __device__ __forceinline__ void pass1(Shared &sh, const uint8_t *__restrict__ fr
 		if (done)
 			store_rec(rec, i, pack_record(w));
 		fc.add(w, caplen, done);
+		if (__ballot(deferred))
+			continue_walk<MODE>(sh, frames, d0, i, fw, w, start_id, sll, rec, g, wq, npend, fc);
 		d0 = d1;
 		d1 = d2;
 	}
 	fc.flush(s_cnt, lane);
-}
-
-// The LINKTYPE_LINUX_SLL head (dissector_sll.c:39-82): pulls nothing; in
-// print_full the next ops come from the packet's sockaddr_ll: a hatype that
-// pcap_devtype_to_linktype (pcap_io.h:205-267) maps to LINKTYPE_EN10MB
-// continues in eth_lay2 with ntohs(sll_protocol) at offset 0, ARPHRD_NETLINK
-// continues with the netlink ops (a host leaf), anything else ends the chain
-// ("[ Unknown protocol ]").  print_less dispatches nothing.
-template <int MODE>
-__device__ __forceinline__ void sll_head(Shared &sh, WalkOut &w, const uint32_t *__restrict__ sll, uint32_t i)
-{
-	const uint32_t w0 = sll ? sll[5 * (size_t)i] : 0u;       // sll_family | sll_protocol << 16
-	const uint32_t w2 = sll ? sll[5 * (size_t)i + 2] : 0u;   // sll_hatype | pkttype << 16 | halen << 24
-	const uint32_t hatype = w2 & 0xFFFF;
-	const uint32_t proto = __builtin_bswap16((uint16_t)(w0 >> 16));
-	w.chain = NSD_OPS_SLL;
-	w.n = 1;
-	atomicAdd(&sh.cnt[NSD_CNT_OPS + NSD_OPS_SLL], 1ull);
-	w.id = sll_next(hatype, proto, MODE, sh.step[32 + NSD_L2H(proto)]);
-}
-
-// The packets pass 1 queued (the block's own queue region), walked with the
-// resumable general walk.  Lanes are refilled: a lane whose chain ends takes
-// the next queued packet (entry and descriptor prefetched two rounds ahead),
-// so every round stages 64 useful windows instead of waiting for the wave's
-// slowest chain.  A round: stage each lane's 64-byte window at its cursor,
-// run layers until every lane has ended its chain or needs bytes past its
-// window, emit the ended ones.  ICMPv4 messages past the window go to the
-// block's pass-2 pending list (sh.pn entries), ext chains to the ext pool.
-template <int MODE>
-__device__ __forceinline__ uint32_t pass2(Shared &sh, const uint8_t *__restrict__ frames,
-				      const uint64_t *__restrict__ desc, int start_id, uint4 *__restrict__ rec,
-				      const uint4 *__restrict__ queue, uint32_t region,
-				      uint64_t *__restrict__ pend2, uint32_t *__restrict__ ext, uint32_t ext_words,
-				      uint32_t *__restrict__ ext_used, uint32_t chunk, uint32_t q0,
-				      const uint32_t *__restrict__ sll)
-{
-	constexpr int ROW = row_of(WIN2);
-	const int lane = threadIdx.x & 63;
-	const int wv = threadIdx.x >> 6;
-	uint64_t *const bp = pend2 + (size_t)blockIdx.x * region;   // this block's pending list
-	const uint32_t nq = sh.qn;
-	const uint4 *const bq = queue + (size_t)blockIdx.x * region;
-	uint32_t *const lay = &sh.lay[wv][0];
-	const GenSink g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, lay };
-	FlagCnt fc;
-
-	bool have = false;            // the lane is walking a packet
-	WalkOut w;
-	walk_init(w, 0, 0);
-	uint32_t i = 0, caplen = 0, m = 0, wb = 0;
-	uint64_t d = 0;
-	uint4 pe = make_uint4(0, 0, 0, 0);   // prefetched queue entry
-	uint64_t pd = 0;                      // its descriptor
-	bool pa = false, pb = false;          // entry in flight / entry + descriptor in flight
-	bool drained = nq <= q0;              // wave-uniform: no queue entries left to take
-
-	for (;;) {
-		// (1) a lane without a packet takes its prefetched one
-		const bool take = !have && pb;
-		if (take) {
-			i = pe.x;
-			d = pd;
-			caplen = NSD_DESC_CAPLEN(d);
-			m = (uint32_t)NSD_DESC_OFF(d) & 15;
-			if (pe.z >> 31) {
-				// resume where pass 1 stopped: Ethernet, tags, IP recorded
-				walk_init(w, caplen, (int)((pe.z >> 20) & 31));
-				w.data = pe.y & 0xFFFF;
-				w.tail = pe.y >> 16;
-				w.chain = pe.z & 0xFFFFF;
-				w.n = (pe.z >> 25) & 7;
-				w.ip_csum = (uint16_t)pe.w;
-#pragma unroll
-				for (uint32_t k = 1; k < 4; k++)
-					if (k < w.n)   // layer k >= 1 of a fast-path chain starts at 14 + 4(k-1)
-						w.offA |= (uint64_t)(14 + 4 * (k - 1)) << (16 * k);
-#pragma unroll
-				for (uint32_t k = 0; k < 4; k++)
-					if (k < w.n)
-						atomicAdd(&sh.cnt[NSD_CNT_OPS + ((w.chain >> (5 * k)) & 31)], 1ull);
-			} else {
-				walk_init(w, caplen, start_id);
-				if (start_id == NSD_OPS_SLL)
-					sll_head<MODE>(sh, w, sll, i);
-			}
-			wb = (w.data + m) & ~15u;
-			have = true;
-			pb = false;
-		}
-		// (2) an entry that arrived in an earlier round: fetch its descriptor
-		if (pa && !pb) {
-			pd = desc[pe.x];
-			pb = true;
-			pa = false;
-		}
-		// (3) a lane with nothing prefetched takes the next queue entry
-		const bool want = !pa && !pb && !drained;
-		const uint64_t wm = __ballot(want);
-		if (wm) {
-			const int leader = __ffsll((unsigned long long)wm) - 1;
-			const uint32_t cnt = (uint32_t)__popcll(wm);
-			uint32_t qb = 0;
-			if (lane == leader)
-				qb = atomicAdd(&sh.q2, cnt);
-			qb = __shfl(qb, leader, 64);
-			const uint32_t kq = qb + lanes_below(wm);
-			if (want && kq < nq) {
-				pe = bq[kq];
-				pa = true;
-			}
-			drained = qb + cnt >= nq;
-		}
-		if (!__ballot(have)) {
-			if (!__ballot(pa || pb))
-				break;
-			continue;
-		}
-		// (4) stage every walking lane's window at its cursor
-		Chunks<WIN2> ch;
-		stage_load<true, WIN2>(ch, frames, d, wb | (have ? 0u : 0x80000000u), lane);
-		stage_write(&sh.win[wv][0], ch, lane);
-		wave_sync_lds();
-		// (5) layers until each lane ends its chain or needs bytes past its window
-		const LSrc<false, WIN2> src{ &sh.win[wv][lane * ROW], sh.lay3, sh.step, frames + NSD_DESC_OFF(d),
-					     caplen, m, wb, false };
-		bool susp;
-		for (;;) {
-			const bool run = have && w.id != 0;
-			susp = run && src.near_end(w.data, w.id);
-			const bool act = run && !susp;
-			if (!__ballot(act))
-				break;
-			gen_step<MODE>(src, act, w, g);
-		}
-		wave_sync_lds();
-		// (6) emit the lanes whose chain ended
-		const bool fin = have && !susp;
-		if (MODE == PRINT_NORM) {
-			const bool pnd = fin && w.icmp_pend;
-			const uint64_t pm = __ballot(pnd);
-			if (pm) {
-				const int leader = __ffsll((unsigned long long)pm) - 1;
-				uint32_t pb0 = 0;
-				if (lane == leader)
-					pb0 = atomicAdd(&sh.pn, (uint32_t)__popcll(pm));
-				pb0 = __shfl(pb0, leader, 64);
-				if (pnd)
-					bp[pb0 + lanes_below(pm)] = pend_entry(i, w.icmp_off, w.icmp_len);
-			}
-		}
-		// ext chains: a pool entry (unless a deep chain took one already):
-		// header, layers 0..5 from the record registers, 6..15 from the
-		// LDS list (deeper ones are in the entry already)
-		const bool ex = fin && w.need_ext;
-		if (__ballot(ex)) {
-			const bool tk = ex && !w.ext_on;
-			const uint32_t sb = ext_take(g, tk, NSD_EXT_WORDS(NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS));
-			if (tk) {
-				w.slot = sb;
-				w.ext_on = true;
-			}
-			if (ex && w.slot == 0xFFFFFFFFu)
-				w.flags |= NSD_F_OVERFLOW;   // the pool is full
-			if (ex && w.slot != 0xFFFFFFFFu) {
-				uint32_t *e = ext + w.slot;
-				const uint32_t nl = w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS;
-				auto lv = [&](uint32_t j) -> uint32_t {
-					if (j < NSD_REC_MAX_LAYERS)
-						return ((w.chain >> (5 * j)) & 31) | (uint32_t)off_of(w, j) << 16;
-					return j < nl ? lay[(j - NSD_REC_MAX_LAYERS) * 64 + lane] : 0u;
-				};
-				*(uint4 *)e = make_uint4(i, nl, 0, 0);
-				*(uint4 *)(e + 4) = make_uint4(lv(0), lv(1), lv(2), lv(3));
-				if (nl > 4)
-					*(uint4 *)(e + 8) = make_uint4(lv(4), lv(5), lv(6), lv(7));
-				if (nl > 8)
-					*(uint4 *)(e + 12) = make_uint4(lv(8), lv(9), lv(10), lv(11));
-				if (nl > 12)
-					*(uint4 *)(e + 16) = make_uint4(lv(12), lv(13), lv(14), lv(15));
-			}
-		}
-		if (fin)
-			store_rec(rec, i, pack_record(w));
-		fc.add(w, caplen, fin);
-		have = have && susp;
-		if (susp)
-			wb = (w.data + m) & ~15u;
-	}
-	fc.flush(sh.cnt, lane);
-	return nq;
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
@@ -724,17 +632,15 @@ __device__ __forceinline__ uint32_t pass2(Shared &sh, const uint8_t *__restrict_
 template <int U>
 __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict__ frames,
 					  const uint64_t *__restrict__ desc, uint4 *__restrict__ rec,
-					  const uint64_t *__restrict__ pend, const uint64_t *__restrict__ pend2,
-					  uint32_t region)
+					  const uint64_t *__restrict__ pend, uint32_t region)
 {
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
 	const uint32_t sub = lane & 3, grp = lane >> 2;
 	uint32_t bad = 0;
-	for (int l = 0; l < PLISTS; l++) {
-		const uint32_t cnt = l < WAVES ? sh.pcnt[l] : sh.pn;
-		const uint64_t *list = l < WAVES ? pend + ((size_t)blockIdx.x * WAVES + l) * (region / WAVES)
-						 : pend2 + (size_t)blockIdx.x * region;
+	for (int l = 0; l < WAVES; l++) {
+		const uint32_t cnt = sh.pcnt[l];
+		const uint64_t *list = pend + ((size_t)blockIdx.x * WAVES + l) * (region / WAVES);
 		// the block's waves split each list in 64-entry pieces
 		for (uint32_t k0 = 64 * ((wv + l) % WAVES); k0 < cnt; k0 += 64 * WAVES) {
 			const bool on = k0 + lane < cnt;
@@ -790,68 +696,43 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 		atomicAdd(&sh.cnt[NSD_CNT_ICMP_BAD], (unsigned long long)bad);
 }
 
-// One launch per batch.  Each block of the persistent grid runs, in order:
-// pass 1 over its grid-stride tiles, pass 2 over the packets it queued, and
-// the ICMPv4 checksums it left pending.  Every later phase reads only what
-// the same block wrote (its queue region and pending lists), so the phases
-// need block barriers, not grid-wide ones, and a block's pass 2 / checksum
-// work overlaps other blocks' pass 1.
+// One launch per batch.  Each block of the persistent grid walks its
+// grid-stride tiles (fast walk + continuations), then sums the ICMPv4
+// messages its waves left pending; a later phase reads only what the same
+// block wrote (its pending lists), so the phases need a block barrier, not a
+// grid-wide one.
 template <int MODE>
 __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 	uint4 *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
-	uint4 *__restrict__ queue, uint32_t region, uint64_t *__restrict__ pend,
-	uint64_t *__restrict__ pend2, const uint32_t *__restrict__ sll)
+	uint64_t *__restrict__ pend, uint32_t region, const uint32_t *__restrict__ sll)
 {
 	__shared__ Shared sh;
-	if (threadIdx.x == 0) {
-		sh.qn = 0;
-		sh.pn = 0;
-		sh.q2 = 0;
-	}
 	if (threadIdx.x < 64)
 		sh.step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h.e[threadIdx.x - 32];
 	if (threadIdx.x < 2 * WAVES)
 		sh.wc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
 	block_init(sh.cnt, sh.lay3);   // (its barrier orders the stores above too)
 
-	// Pass 1 and pass 2 alternate over spans of NSD_P1_TILES grid strides, so
-	// a deferred packet is restaged while the lines pass 1 read are still in
-	// L2 / MALL (a whole-shard pass 1 first evicts them).
-	const uint32_t stride = gridDim.x * BLOCK;
-	const uint64_t span = NSD_P1_TILES ? (uint64_t)NSD_P1_TILES * stride : (uint64_t)n;
-	uint32_t npend = 0, q0 = 0;
-	for (uint64_t c0 = 0; c0 < n; c0 += span) {
-		const uint32_t end = (uint32_t)(c0 + span < n ? c0 + span : n);
-		pass1<MODE>(sh, frames, desc, n, start_id, rec, queue, region, pend, (uint32_t)c0, end, npend);
-		if (MODE == PRINT_NORM || MODE == PRINT_LESS) {
-			__syncthreads();   // the span's queue entries and sh.qn are complete
-			// (waves take queue entries dynamically and pass 2 has no block
-			// barrier, so fewer walkers only changes who drains the queue)
-			if ((threadIdx.x >> 6) < NSD_P2_WAVES)
-				q0 = pass2<MODE>(sh, frames, desc, start_id, rec, queue, region, pend2, ext,
-						 ext_words, ext_used, chunk, q0, sll);
-			__syncthreads();   // every wave is done taking entries: restart the taker at q0
-			if (threadIdx.x == 0)
-				sh.q2 = q0;
-		}
-	}
+	uint32_t npend = 0;
+	walk_tiles<MODE>(sh, frames, desc, n, start_id, rec, pend, region, ext, ext_words, ext_used, chunk, sll,
+			 npend);
 	if ((threadIdx.x & 63) == 0)
 		sh.pcnt[threadIdx.x >> 6] = npend;
 	if (MODE == PRINT_NORM) {
 		__syncthreads();   // records final, pending lists and counts complete
-		icmp_pass<NSD_CSUM_U>(sh, frames, desc, rec, pend, pend2, region);
+		icmp_pass<NSD_CSUM_U>(sh, frames, desc, rec, pend, region);
 	}
 	block_flush(sh.cnt, counters);
 }
 
+
 } // namespace nsd
 
 // ---- launcher (C ABI, called by nsd_host.cpp / nsd_pipe.cpp) -----------------
-// A persistent grid of at most NSD_MAX_GRID blocks; block b owns queue
-// region b and pending lists b (room for every packet it
-// visits).
+// A persistent grid of at most NSD_MAX_GRID blocks; block b owns pending
+// lists b (room for every packet it visits).
 constexpr uint32_t NSD_MAX_GRID = 4096;
 
 static uint32_t region_for(uint32_t n, uint32_t blocks)
@@ -866,11 +747,10 @@ static size_t region_slots(uint32_t n)
 	return ((size_t)n + (size_t)NSD_MAX_GRID * nsd::BLOCK + 1) & ~(size_t)1;
 }
 
-// workspace: the deferral queue (uint4 per slot), the pass-1 and pass-2
-// pending-checksum lists (u64 per slot)
+// workspace: the pending-checksum lists (u64 per slot)
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
-	return (16 + 8 + 8) * region_slots(n);
+	return 8 * region_slots(n);
 }
 
 extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
@@ -926,9 +806,7 @@ extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d
 	if (blocks > cap_blocks)
 		blocks = cap_blocks;
 	const uint32_t region = region_for(n, blocks);
-	uint4 *queue = (uint4 *)d_ws;
-	uint64_t *pend = (uint64_t *)(queue + region_slots(n));
-	uint64_t *pend2 = pend + region_slots(n);
+	uint64_t *pend = (uint64_t *)d_ws;
 	// ext pool chunk per request: half the pool spread over the waves, so the
 	// unused chunk tails the waves keep at the end waste at most half of it
 	// (a pool of 2x the words the chains need never overflows), within
@@ -941,6 +819,6 @@ extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d
 	hipLaunchKernelGGL(mi == 0 ? dissect_all<PRINT_NORM> : mi == 1 ? dissect_all<PRINT_LESS> : dissect_all<PRINT_HEX>,
 			   dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id,
 			   (uint4 *)d_rec, d_ext, ext_words, d_ext_used, chunk, (unsigned long long *)d_counters,
-			   queue, region, pend, pend2, (const uint32_t *)d_sll);
+			   pend, region, (const uint32_t *)d_sll);
 	return hipGetLastError() == hipSuccess ? 0 : -2;
 }
