@@ -122,8 +122,9 @@ typedef struct nsd_rec {
 #define NSD_REC_MAX_LAYERS   6
 #define NSD_N_EXT            7
 #define NSD_F_ICMP_BAD       0x08  /* ICMPv4 checksum nonzero: "bogus (!)" (proto_icmpv4.c:74-81) */
-#define NSD_F_HOST           0x10  /* last layer's body is rendered by the host (ICMPv6 130-154,
-                                      ARP, LLDP, IGMP, DCCP, non-Ethernet link types) */
+#define NSD_F_HOST           0x10  /* last layer's fields are printed by the host renderer
+                                      (ICMPv6 130-154, ARP, LLDP, IGMP, DCCP, non-Ethernet link
+                                      types); data_off is still where that parser's pulls end */
 #define NSD_F_OVERFLOW       0x20  /* chain longer than NSD_EXT_MAX_LAYERS or ext pool full:
                                       record holds the first layers only */
 

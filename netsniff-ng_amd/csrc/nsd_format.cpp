@@ -1046,12 +1046,9 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 		if (!dn.ok)
 			return NSD_ERR_FORMAT;
 		// consistency with the record: next layer's start / final cursor
+		// (for a host-rendered leaf too: the walk kept where its pulls end)
 		if (k + 1 < n) {
 			if (!dn.next || dn.data != offs[k + 1])
-				return NSD_ERR_FORMAT;
-		} else if (host) {
-			// a host-rendered leaf: the device left the cursor at its start
-			if (dn.next || L.start != rec.data_off || dn.tail != rec.tail_off)
 				return NSD_ERR_FORMAT;
 		} else {
 			if (dn.next || dn.data != rec.data_off || dn.tail != rec.tail_off)

@@ -62,6 +62,14 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
 	return v;
 }
 
+// The frame's bytes straight from HBM (zero past caplen), for the leaf walks
+struct HbmBytes {
+	const uint8_t *p;
+	uint32_t caplen;
+	__device__ __forceinline__ uint8_t b(uint32_t o) const { return o < caplen ? p[o] : 0; }
+	__device__ __forceinline__ uint16_t be16(uint32_t o) const { return (uint16_t)(b(o) << 8 | b(o + 1)); }
+};
+
 // Byte source over an LDS window (aligned coordinates, see top).
 // FAST: bytes outside the window are not fetched; the source records the
 // miss and the walk gives the packet up to pass 2.  Otherwise they come from
@@ -391,16 +399,38 @@ __device__ __forceinline__ void sll_head(Shared &sh, WalkOut &w, const uint32_t 
 	w.id = sll_next(hatype, proto, MODE, sh.step[32 + NSD_L2H(proto)]);
 }
 
+// A wave's pending list (wq, `wcap` slots: one per packet the wave visits)
+// holds the ICMPv4 checksums left to icmp_pass from the front (npend) and
+// the host-rendered leaves left to leaf_pass from the back (nleaf); a packet
+// ends in at most one of the two.
+struct Pending {
+	uint64_t *wq;
+	uint32_t wcap;
+	uint32_t npend, nleaf;
+};
+
+// leaf entry: packet index | leaf start << 32 | ops id << 48
+__device__ __forceinline__ uint64_t leaf_entry(uint32_t i, uint32_t start, int id)
+{
+	return (uint64_t)i | (uint64_t)(start & 0xFFFF) << 32 | (uint64_t)id << 48;
+}
+
 // What a lane whose general walk ended leaves behind (wave-uniform call):
-// an ICMPv4 message past its windows goes to the wave's pending list, an ext
-// chain to the pool (layers 0..5 from the record registers, 6..15 from the
-// wave's LDS list, deeper ones already in the entry), then the record and the
-// flag counts.
+// an ICMPv4 message past its windows and a host-rendered leaf go to the
+// wave's pending list, an ext chain to the pool (layers 0..5 from the record
+// registers, 6..15 from the wave's LDS list, deeper ones already in the
+// entry), then the record and the flag counts.
 template <int MODE>
 __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, uint32_t caplen, const GenSink &g,
-					     uint4 *__restrict__ rec, uint64_t *__restrict__ wq, uint32_t &npend,
-					     FlagCnt &fc, int lane)
+					     uint4 *__restrict__ rec, Pending &pq, FlagCnt &fc, int lane)
 {
+	const bool lf = fin && w.leaf != 0;
+	const uint64_t lm = __ballot(lf);
+	if (lf)
+		pq.wq[pq.wcap - 1 - (pq.nleaf + lanes_below(lm))] = leaf_entry(i, w.data, w.leaf);
+	pq.nleaf += (uint32_t)__popcll(lm);
+	uint64_t *const wq = pq.wq;
+	uint32_t &npend = pq.npend;
 	if (MODE == PRINT_NORM) {
 		const bool pnd = fin && w.icmp_pend;
 		const uint64_t pm = __ballot(pnd);
@@ -458,7 +488,7 @@ template <int MODE>
 __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restrict__ frames, uint64_t d,
 					      uint32_t i, uint32_t fw, WalkOut &w, int start_id,
 					      const uint32_t *__restrict__ sll, uint4 *__restrict__ rec,
-					      const GenSink &g, uint64_t *__restrict__ wq, uint32_t &npend, FlagCnt &fc)
+					      const GenSink &g, Pending &pq, FlagCnt &fc)
 {
 	constexpr int ROW = row_of(WIN2);
 	const int lane = threadIdx.x & 63;
@@ -496,7 +526,7 @@ __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restr
 			gen_step<MODE>(src, act, w, g);
 		}
 		wave_sync_lds();
-		emit_general<MODE>(have && !susp, w, i, caplen, g, rec, wq, npend, fc, lane);
+		emit_general<MODE>(have && !susp, w, i, caplen, g, rec, pq, fc, lane);
 		have = have && susp;
 		if (susp)
 			wb = (w.data + m) & ~15u;
@@ -507,13 +537,13 @@ __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restr
 // Every packet of the block's grid-stride tiles, one wave per 64-packet tile:
 // the fast walk over each packet's first 64 bytes, then the general walk
 // for the lanes it could not finish (continue_walk); ICMPv4 messages past
-// the windows go to the wave's pending list (npend entries).
+// the windows and host-rendered leaves go to the wave's pending list (pq).
 template <int MODE>
 __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict__ frames,
 					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
-					   uint4 *__restrict__ rec, uint64_t *__restrict__ pend, uint32_t region,
-					   uint32_t *__restrict__ ext, uint32_t ext_words, uint32_t *__restrict__ ext_used,
-					   uint32_t chunk, const uint32_t *__restrict__ sll, uint32_t &npend)
+					   uint4 *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
+					   uint32_t *__restrict__ ext_used, uint32_t chunk,
+					   const uint32_t *__restrict__ sll, Pending &pq)
 {
 	constexpr int ROW = row_of(WIN1);
 	auto &s_win = sh.win;
@@ -523,8 +553,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	const int wv = threadIdx.x >> 6;
 
 	const uint32_t stride = gridDim.x * BLOCK;
-	// this wave's pending-checksum list (a wave visits region / WAVES packets)
-	uint64_t *const wq = pend + ((size_t)blockIdx.x * WAVES + wv) * (region / WAVES);
+	uint64_t *const wq = pq.wq;
 	const GenSink g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, &sh.lay[wv][0] };
 	FlagCnt fc;
 	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
@@ -585,8 +614,8 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			const bool pnd = w.icmp_pend && done;
 			const uint64_t pmask = __ballot(pnd);
 			if (pnd)
-				wq[npend + lanes_below(pmask)] = pend_entry(i, w.icmp_off, w.icmp_len);
-			npend += (uint32_t)__popcll(pmask);
+				wq[pq.npend + lanes_below(pmask)] = pend_entry(i, w.icmp_off, w.icmp_len);
+			pq.npend += (uint32_t)__popcll(pmask);
 		}
 		// per-ops counts from the finished chains, grouped by chain word
 		// (ids are >= 1, so equal chain words imply equal layer counts)
@@ -613,7 +642,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			store_rec(rec, i, pack_record(w));
 		fc.add(w, caplen, done);
 		if (__ballot(deferred))
-			continue_walk<MODE>(sh, frames, d0, i, fw, w, start_id, sll, rec, g, wq, npend, fc);
+			continue_walk<MODE>(sh, frames, d0, i, fw, w, start_id, sll, rec, g, pq, fc);
 		d0 = d1;
 		d1 = d2;
 	}
@@ -696,11 +725,38 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 		atomicAdd(&sh.cnt[NSD_CNT_ICMP_BAD], (unsigned long long)bad);
 }
 
+// ---- host-rendered leaves -------------------------------------------------------
+// The leaves the wave's general walk ended in (ARP / LLDP / IGMP / DCCP /
+// ICMPv6 130-154; ARP and DCCP inside the fast window finish in fast_walk):
+// one lane per entry walks the leaf parser's pulls over the frame in HBM
+// (nsd_leaf.h) and rewrites the record's cursor word.  A pass of its own,
+// after the tiles, so the LLDP TLV and ND-option loops do not add to the
+// walk's register peak.  The wave reads back only what it wrote itself.
+template <int MODE>
+__device__ __forceinline__ void leaf_pass(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc,
+					  uint4 *__restrict__ rec, const Pending &pq)
+{
+	if (!pq.nleaf)
+		return;
+	__threadfence();   // the wave's record and list stores complete before its loads below
+	for (uint32_t k = threadIdx.x & 63; k < pq.nleaf; k += 64) {
+		const uint64_t e = pq.wq[pq.wcap - 1 - k];
+		const uint32_t i = (uint32_t)e, start = (uint32_t)(e >> 32) & 0xFFFF;
+		const int id = (int)(e >> 48);
+		const uint64_t d = desc[i];
+		uint32_t *const y = (uint32_t *)(rec + i) + 1;   // data_off | tail_off << 16
+		const uint32_t tail = __hip_atomic_load(y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16;
+		const uint32_t end =
+			leaf_end<MODE>(HbmBytes{ frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d) }, id, start, tail);
+		*y = end | tail << 16;
+	}
+}
+
 // One launch per batch.  Each block of the persistent grid walks its
-// grid-stride tiles (fast walk + continuations), then sums the ICMPv4
-// messages its waves left pending; a later phase reads only what the same
-// block wrote (its pending lists), so the phases need a block barrier, not a
-// grid-wide one.
+// grid-stride tiles (fast walk + continuations), walks the leaves its waves
+// left pending, then sums the ICMPv4 messages they left pending; a later
+// phase reads only what the same block wrote (its pending lists), so the
+// phases need a block barrier, not a grid-wide one.
 template <int MODE>
 __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
@@ -715,11 +771,14 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 		sh.wc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
 	block_init(sh.cnt, sh.lay3);   // (its barrier orders the stores above too)
 
-	uint32_t npend = 0;
-	walk_tiles<MODE>(sh, frames, desc, n, start_id, rec, pend, region, ext, ext_words, ext_used, chunk, sll,
-			 npend);
+	// this wave's pending list (a wave visits region / WAVES packets)
+	Pending pq{ pend + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (region / WAVES), region / WAVES, 0,
+		    0 };
+	walk_tiles<MODE>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq);
+	if (MODE == PRINT_NORM || MODE == PRINT_LESS)
+		leaf_pass<MODE>(frames, desc, rec, pq);
 	if ((threadIdx.x & 63) == 0)
-		sh.pcnt[threadIdx.x >> 6] = npend;
+		sh.pcnt[threadIdx.x >> 6] = pq.npend;
 	if (MODE == PRINT_NORM) {
 		__syncthreads();   // records final, pending lists and counts complete
 		icmp_pass<NSD_CSUM_U>(sh, frames, desc, rec, pend, region);

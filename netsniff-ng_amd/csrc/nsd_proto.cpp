@@ -74,7 +74,9 @@ int tty_cols()
 }
 
 // one piece of text, as one or more tprintf calls: the reference's buffer is
-// 1 KiB and panics on a single call longer than that (tprintf.c:126-162)
+// 1 KiB and panics on a single call longer than that (tprintf.c:126-162).
+// A NUL byte (a "%c" of packet data, e.g. proto_icmpv6.c:563) goes in as
+// its own "%c" call: "%.*s" would stop at it
 void out(const char *p, size_t n)
 {
 	if (!n)
@@ -84,9 +86,15 @@ void out(const char *p, size_t n)
 		return;
 	}
 	if (tprintf) {
-		for (size_t i = 0; i < n; i += 256) {
-			const size_t k = n - i < 256 ? n - i : 256;
+		for (size_t i = 0; i < n;) {
+			if (!p[i]) {
+				tprintf((char *)"%c", 0);
+				i++;
+				continue;
+			}
+			size_t k = strnlen(p + i, n - i < 256 ? n - i : 256);
 			tprintf((char *)"%.*s", (int)k, p + i);
+			i += k;
 		}
 		return;
 	}
@@ -221,14 +229,7 @@ void run_layer(struct pkt_buff *pkt, int id, int mode)
 	if (!nsd::render_layer(s, head, caplen, id, start, tail, mode, csum, flags & NSD_F_ICMP_BAD, sll, rdata,
 			       rtail, rnext))
 		bug("layer cannot be rendered", id);
-	if (flags & NSD_F_HOST) {
-		// a leaf whose pulls only the renderer follows (ARP, LLDP, IGMP,
-		// DCCP, ICMPv6 130-154 bodies): the walk left the cursor at its start
-		if (next || rnext)
-			bug("host-rendered leaf chains on", id);
-		data = rdata;
-		ntail = rtail;
-	} else if (rdata != data || rtail != ntail || rnext != (next != 0)) {
+	if (rdata != data || rtail != ntail || rnext != (next != 0)) {
 		bug("walk and renderer disagree on the layer's end", id);
 	}
 	out(s);

@@ -22,6 +22,8 @@
 
 #define NSD_HD __host__ __device__ __forceinline__
 
+#include "nsd_leaf.h"
+
 namespace nsd {
 
 // dissector_eth.c:30-39 (eth_lay2): exact-key map -> ops id
@@ -78,6 +80,7 @@ struct WalkOut {
 	int      id;         // next ops to run (0 = chain ended)
 	bool     icmp_pend;  // ICMPv4 checksum left to the wave-cooperative pass
 	uint32_t icmp_off, icmp_len;
+	int      leaf;       // device: a host-rendered leaf at w.data whose end is still to walk
 };
 
 // Where the general walk puts what it records beyond the 16-byte record:
@@ -101,6 +104,13 @@ struct GenSink {
 	__device__ __forceinline__ void take_deep(bool deep_first, WalkOut &w) const;
 	// count layer k (ops id, start offset) and keep it beyond the record
 	__device__ __forceinline__ void layer(const WalkOut &w, uint32_t k, int id, uint32_t start) const;
+	// a host-rendered leaf ends the chain: its pulls are walked once the
+	// lane's chain is done (emit_general), where fewer registers are live
+	template <int MODE, class Src>
+	__device__ __forceinline__ void leaf(const Src &, bool lw, WalkOut &w, int id, uint32_t) const
+	{
+		w.leaf = lw ? id : w.leaf;
+	}
 };
 
 // Wave-uniform call: every lane with `want` gets a pool entry of `words`
@@ -182,6 +192,12 @@ struct HostSink {
 		if (counters)
 			counters[NSD_CNT_OPS + id]++;
 	}
+	template <int MODE, class Src>
+	__host__ void leaf(const Src &s, bool lw, WalkOut &w, int id, uint32_t start) const
+	{
+		if (lw)
+			w.data = leaf_end<MODE>(s, id, start, w.tail);
+	}
 };
 
 NSD_HD uint16_t off_of(const WalkOut &w, uint32_t k)
@@ -217,6 +233,7 @@ NSD_HD void walk_init(WalkOut &w, uint32_t caplen, int start_id)
 	w.icmp_pend = false;
 	w.icmp_off = 0;
 	w.icmp_len = 0;
+	w.leaf = 0;
 }
 
 // Per-ops step table for the general walk: the first pull (minl), the fixed
@@ -421,6 +438,10 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	w.data = upd ? start + (pulled ? adv : 0u) : w.data;
 	w.id = upd ? ((pulled & cont) ? nx : 0) : w.id;
 	w.flags |= (upd & host) ? NSD_F_HOST : 0;
+	// a host-rendered leaf: where its parser's pulls leave the cursor
+	// (nsd_leaf.h), so the exit op's dump starts from the record; the
+	// sink decides when (the device walks it after the chain, emit_general)
+	g.template leaf<MODE>(s, upd & host, w, id, start);
 	if (MODE == PRINT_NORM) {
 		// tail trim to tot_len - ihl*4, evaluated in size_t (:174-175)
 		const int64_t x = (int64_t)k2 - (int64_t)ihl * 4;
@@ -473,11 +494,12 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 
 // Straight-line walk for the common chains (pass 1): Ethernet, up to two
 // 802.1Q / 802.1ad tags, IPv4 or IPv6, then TCP / UDP / ICMPv4 / ICMPv6 /
-// ESP / NoNext (or a host-rendered leaf: ARP, LLDP, IGMP, DCCP).  Same
-// semantics as gen_step() for every packet it finishes (the c_step table
-// cites the reference per ops); anything else (MPLS, deeper tag stacks,
-// extension headers, IPv6-in-IPv4, bytes past the staged window) goes to
-// pass 2.  No loop, no per-layer dispatch switch.
+// ESP / NoNext (or the host-rendered leaves ARP and DCCP).  Same semantics
+// as gen_step() for every packet it finishes (the c_step table cites the
+// reference per ops); anything else (MPLS, deeper tag stacks, extension
+// headers, IPv6-in-IPv4, the looping leaves LLDP / IGMP / ICMPv6 130-154,
+// bytes past the staged window) goes to pass 2.  No loop, no per-layer
+// dispatch switch.
 // Returns FW_DONE, FW_RESTART (pass 2 walks the packet from its start) or
 // FW_RESUME (the chain reached an extension header / AH / IPv6-in-IPv4 ops
 // at w.data with layers 0..w.n-1 recorded: pass 2 resumes there with w.id).
@@ -550,11 +572,19 @@ __device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, Wal
 		}
 		d2 = d + 40;
 		l4 = s.lay3(s.b(d + 6));
-	} else if (next == NSD_OPS_ARP || next == NSD_OPS_LLDP) {
+	} else if (next == NSD_OPS_ARP) {
 		rec(next, d);
 		w.flags |= NSD_F_HOST;
+		w.data = leaf_arp(s, d, caplen);
 		w.n = n;
 		return s.missed() ? FW_RESTART : FW_DONE;
+	} else if (next == NSD_OPS_LLDP) {
+		// the TLV walk reads past the window: the general walk runs it
+		if (s.missed())
+			return FW_RESTART;
+		w.n = n;
+		w.id = next;
+		return FW_RESUME;
 	} else if (next == 0) {
 		w.n = n;
 		return s.missed() ? FW_RESTART : FW_DONE;
@@ -594,27 +624,27 @@ __device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, Wal
 			}
 		}
 		break;
-	case NSD_OPS_ICMPV6:
+	case NSD_OPS_ICMPV6: {
+		const uint8_t type = s.b(d2);
+		if (MODE == PRINT_NORM && len >= 4 && type >= 130 && type <= 154)
+			goto resume;   // variable-length bodies (MLD, ND options, ...)
 		rec(l4, d2);
 		if (len >= 4) {
 			w.data = d2 + 4;
-			if (MODE == PRINT_NORM) {
-				const uint8_t type = s.b(d2);
-				if (type >= 130 && type <= 154) {
-					w.flags |= NSD_F_HOST;
-					w.data = d2;
-				} else if (((type >= 1 && type <= 4) || type == 128 || type == 129) && len - 4 >= 4) {
-					w.data = d2 + 8;
-				}
-			}
+			if (MODE == PRINT_NORM && ((type >= 1 && type <= 4) || type == 128 || type == 129) &&
+			    len - 4 >= 4)
+				w.data = d2 + 8;
 		}
 		break;
-	case NSD_OPS_IGMP:
+	}
 	case NSD_OPS_DCCP:
 		rec(l4, d2);
 		w.flags |= NSD_F_HOST;
+		w.data = leaf_dccp(s, d2, w.tail, MODE);
 		break;
 	default:
+	resume:
+		// IGMP (its v3 lists run past the window), the ICMPv6 bodies above,
 		// extension headers, AH, IPv6-in-IPv4: pass 2 resumes at d2
 		if (s.missed())
 			return FW_RESTART;

@@ -1206,6 +1206,8 @@ static void icmpv6_process(uint8_t type, uint8_t code, const char **ts, const ch
 	}
 }
 
+static void C_icmpv6_body(P *k);
+
 /* icmpv6 / icmpv6_less (proto_icmpv6.c:1667-1699): leaf */
 static int L_icmpv6(P *k, uint32_t layer_start)
 {
@@ -1225,9 +1227,11 @@ static int L_icmpv6(P *k, uint32_t layer_start)
 		int body;
 		icmpv6_process(type, code, &ts, &cs, &body);
 		if (body < 0) {
-			/* variable-length body: rendered on the host (NSD_F_HOST) */
+			/* variable-length body: rendered on the host (NSD_F_HOST);
+			 * the walk keeps where its pulls end */
 			k->host = 1;
 			k->data = layer_start;
+			C_icmpv6_body(k);
 			if (k->t)
 				k->t->unsupported = 1;
 			return 0;
@@ -1376,6 +1380,346 @@ static int L_sll(P *k)
 	return 0;
 }
 
+/* ---- host-rendered leaves: the pulls only ---------------------------------
+ * The text of ARP, DCCP, IGMP, LLDP and the ICMPv6 130-154 bodies is the
+ * host renderer's (pinned by the reference objects' goldens); the walk
+ * records where each parser leaves the cursor, which the exit op's dump
+ * starts from.  A failed pull does not advance (pkt_buff.h:43-57). */
+
+/* arp (proto_arp.c:80-196) / arp_less: one struct arphdr */
+static void C_arp(P *k)
+{
+	pull(k, 28, NULL);
+}
+
+/* dccp (proto_dccp.c:70-133) / dccp_less (:135-148) */
+static void C_dccp(P *k)
+{
+	uint32_t h;
+	uint8_t b8;
+
+	if (!pull(k, 12, &h) || k->mode != PRINT_NORM)
+		return;
+	b8 = B(k, h + 8);                  /* x: bit 0, type: bits 1..4 */
+	if ((b8 & 1) && !pull(k, 4, NULL))
+		return;
+	if (((b8 >> 1) & 15) >= 1 && ((b8 >> 1) & 15) <= 9)
+		pull(k, (b8 & 1) ? 8 : 4, NULL);
+}
+
+/* the v3 source list: n pulls of 4 bytes, ending at the first that fails
+ * (proto_igmp.c:368-383, 430-445) */
+static void C_igmp_sources(P *k, size_t n)
+{
+	while (n--)
+		if (!pull(k, 4, NULL))
+			break;
+}
+
+/* igmp (proto_igmp.c:452-493); igmp_less pulls nothing (:495-554) */
+static void C_igmp(P *k)
+{
+	uint32_t len = pkt_len(k), m;
+	uint8_t t = B(k, k->data);
+	size_t nrec;
+
+	if (k->mode != PRINT_NORM)
+		return;
+	switch (t) {
+	case 0x01: case 0x02: case 0x03: case 0x04:
+	case 0x05: case 0x06: case 0x07: case 0x08:
+		if (len == 20)
+			pull(k, 20, NULL);                 /* dissect_igmp_v0 */
+		return;
+	case 0x11:
+		if (len >= 12) {                           /* v3 query (:334-385) */
+			pull(k, 12, &m);
+			C_igmp_sources(k, BE16(k, m + 10));
+		} else if (len == 8) {
+			pull(k, 8, NULL);                  /* v2 / v1 */
+		}
+		return;
+	case 0x12: case 0xFF: case 0xFE: case 0xFD: case 0xFC: case 0x16: case 0x17:
+		if (len == 8)
+			pull(k, 8, NULL);
+		return;
+	case 0x22:                                         /* v3 report (:387-450) */
+		if (len < 8)
+			return;
+		pull(k, 8, &m);
+		nrec = BE16(k, m + 6);
+		while (nrec--) {
+			uint32_t r;
+			if (!pull(k, 8, &r))
+				break;
+			C_igmp_sources(k, BE16(k, r + 2));
+		}
+		return;
+	}
+}
+
+/* lldp_print_net_addr (proto_lldp.c:88-131): 0 ok, -1 invalid */
+static int C_lldp_addr(const P *k, uint32_t a, uint32_t alen)
+{
+	uint8_t af;
+
+	if (alen < 1)
+		return -1;
+	af = B(k, a);
+	alen--;
+	if ((af == 1 && alen < 4) || (af == 2 && alen < 16) || (af == 6 && alen < 6))
+		return -1;
+	return 0;
+}
+
+/* lldp (proto_lldp.c:161-455) / lldp_less (:457-488).  print_full's `len`
+ * only loses the TLV headers (:187), not the TLV bodies */
+static void C_lldp(P *k)
+{
+	unsigned int len = pkt_len(k), n_tlv = 0, type, tlen;
+	uint32_t h, s;
+
+	if (k->mode != PRINT_NORM) {
+		while (len >= 2) {
+			if (!pull(k, 2, &h))
+				break;
+			type = BE16(k, h) >> 9;
+			tlen = BE16(k, h) & 0x1FF;
+			len -= 2;
+			if (type == 0 || tlen == 0 || len < tlen)
+				break;
+			pull(k, tlen, NULL);
+			len -= tlen;
+		}
+		return;
+	}
+	while (len >= 2) {
+		if (!pull(k, 2, &h))
+			return;
+		type = BE16(k, h) >> 9;
+		tlen = BE16(k, h) & 0x1FF;
+		len -= 2;
+		if (type == 0 && tlen == 0)
+			return;
+		if (len < tlen)
+			return;
+		switch (type) {
+		case 1:                 /* Chassis ID / Port ID (:200-295) */
+		case 2:
+			if (n_tlv != type - 1 || tlen < 2 || !pull(k, tlen, &s))
+				return;
+			if (B(k, s) == (type == 1 ? 4 : 3)) {
+				if (tlen < 7)
+					return;
+			} else if (B(k, s) == (type == 1 ? 5 : 4)) {
+				if (C_lldp_addr(k, s + 1, tlen))
+					return;
+			}
+			break;
+		case 3:                 /* TTL (:296-314) */
+			if (n_tlv != 2 || tlen != 2 || !pull(k, 2, NULL))
+				return;
+			break;
+		case 7:                 /* System capabilities (:348-368) */
+			if (tlen != 4 || !pull(k, 4, NULL))
+				return;
+			break;
+		case 8: {               /* Management address (:369-418) */
+			uint32_t alen, oidlen;
+			if (tlen < 9 || tlen > 167 || !pull(k, tlen, &s))
+				return;
+			alen = B(k, s);
+			if (tlen - 1 < alen || C_lldp_addr(k, s + 1, alen))
+				return;
+			if (tlen - alen < 4)
+				return;
+			oidlen = B(k, s + 1 + alen + 1 + 4);
+			if (tlen - alen - 4 < 3 || tlen - alen - 4 - 3 < oidlen)
+				return;
+			break;
+		}
+		case 127:               /* Organizationally specific (:419-437) */
+			if (tlen < 4 || !pull(k, 4, NULL))
+				return;
+			pull(k, tlen - 4, NULL);
+			break;
+		default:                /* descriptions (:315-347), unknown TLVs (:438-441) */
+			pull(k, tlen, NULL);
+			break;
+		}
+		n_tlv++;
+	}
+}
+
+/* `n` one-byte pulls, as the %x / %c loops of proto_icmpv6.c take them */
+static int C_bytes(P *k, int64_t n)
+{
+	while (n-- > 0)
+		if (!pull(k, 1, NULL))
+			return 0;
+	return 1;
+}
+
+/* print_ipv6_addr_list (proto_icmpv6.c:283-299) */
+static int C_addrs(P *k, uint8_t nr)
+{
+	while (nr--)
+		if (!pull(k, 16, NULL))
+			return 0;
+	return 1;
+}
+
+/* the Neighbor Discovery option bodies (proto_icmpv6.c:372-806): each pulls
+ * its fixed part, then `len -= sizeof(*part)` (ssize_t), a negative
+ * remainder failing after the pull */
+static int C_nd_opt(P *k, uint8_t type, ssize_t len)
+{
+	uint32_t a;
+
+	switch (type) {
+	case 1: case 2:                      /* link-layer address (:372-406) */
+		return C_bytes(k, len);
+	case 3:                              /* prefix information (:408-437) */
+		return pull(k, 30, NULL) && (len -= 30) >= 0;
+	case 4:                              /* redirected header (:439-469) */
+		if (!pull(k, 6, NULL) || (len -= 6) < 0)
+			return 0;
+		return C_bytes(k, len);
+	case 5:                              /* MTU (:471-488) */
+		return pull(k, 6, NULL) && (len -= 6) >= 0;
+	case 9: case 10:                     /* address lists (:490-513) */
+		if (!pull(k, 6, NULL) || (len -= 6) < 0)
+			return 0;
+		return C_addrs(k, (uint8_t)(len / 16));
+	case 15: {                           /* naming (:520-584): packed {u8; size_t} */
+		uint64_t pad = 0;
+		ssize_t name_len;
+		if (!pull(k, 9, &a) || (len -= 9) < 0)
+			return 0;
+		for (int i = 7; i >= 0; i--)
+			pad = pad << 8 | B(k, a + 1 + i);
+		if (pad > (uint64_t)len) {
+			pull(k, (uint32_t)len, NULL);
+			return 1;
+		}
+		name_len = len - (ssize_t)pad;
+		if (!C_bytes(k, name_len))
+			return 0;
+		while (pad--)
+			if (!pull(k, 1, NULL))
+				break;
+		return 1;
+	}
+	case 16:                             /* certificate (:590-626) */
+		if (!pull(k, 2, NULL) || (len -= 2) < 0)
+			return 0;
+		C_bytes(k, len);
+		return 1;
+	case 17:                             /* IP address / prefix (:635-710) */
+		if (!pull(k, 2, NULL) || (len -= 2) < 0)
+			return 0;
+		if (len == 20)
+			return pull(k, 20, NULL);
+		if (len == 16)
+			return pull(k, 16, NULL);
+		C_bytes(k, len);
+		return 1;
+	case 19:                             /* link-layer address (:727-762) */
+		if (!pull(k, 1, NULL) || (len -= 1) < 0)
+			return 0;
+		return C_bytes(k, len);
+	default:                             /* the rest skip the option (:786-806) */
+		pull(k, (uint32_t)len, NULL);
+		return 1;
+	}
+}
+
+/* dissect_neighb_disc_ops (proto_icmpv6.c:808-911) */
+static int C_nd_ops(P *k)
+{
+	while (pkt_len(k)) {
+		uint32_t a;
+		ssize_t payl;
+		if (!pull(k, 2, &a))
+			return 0;
+		payl = (ssize_t)(uint16_t)(B(k, a + 1) * 8) - 2;
+		if (payl > (ssize_t)pkt_len(k) || payl < 0)
+			return 0;
+		if (!C_nd_opt(k, B(k, a), payl))
+			return 0;
+	}
+	return 1;
+}
+
+/* dissect_icmpv6_mcast_rec (proto_icmpv6.c:310-370) */
+static int C_mcast_recs(P *k, uint16_t nr)
+{
+	while (nr--) {
+		uint32_t r;
+		uint16_t aux;
+		if (!pull(k, 20, &r))
+			return 0;
+		aux = (uint16_t)(B(k, r + 1) * 4);
+		if (aux > pkt_len(k) || !C_addrs(k, (uint8_t)BE16(k, r + 2)) || aux > pkt_len(k) ||
+		    !C_bytes(k, aux))
+			return 0;
+	}
+	return 1;
+}
+
+/* icmpv6 (proto_icmpv6.c:1667-1688) for the types whose bodies
+ * icmpv6_process dissects at variable length (130-154, :1023-1474) */
+static void C_icmpv6_body(P *k)
+{
+	uint32_t h, a;
+
+	if (!pull(k, 4, &h))
+		return;
+	switch (B(k, h)) {
+	case 130:                                    /* MLD query, MLDv2 (:1023-1070) */
+		if (pull(k, 20, NULL) && pkt_len(k) >= 4 && pull(k, 4, &a))
+			C_addrs(k, (uint8_t)BE16(k, a + 2));
+		break;
+	case 131: case 132:                          /* :1072-1094 */
+		pull(k, 20, NULL);
+		break;
+	case 133: case 141: case 142: case 147: case 148: case 154:
+		if (pull(k, 4, NULL))                /* :1096-1108, 1292-1300, 1355-1386, 1460-1474 */
+			C_nd_ops(k);
+		break;
+	case 134:                                    /* :1110-1127 */
+		if (pull(k, 12, NULL))
+			C_nd_ops(k);
+		break;
+	case 135: case 136:                          /* :1129-1167 */
+		if (pull(k, 20, NULL))
+			C_nd_ops(k);
+		break;
+	case 137:                                    /* :1169-1188 */
+		if (pull(k, 36, NULL))
+			C_nd_ops(k);
+		break;
+	case 138: case 139: case 140:                /* :1210-1279 */
+		pull(k, 12, NULL);
+		break;
+	case 143:                                    /* MLDv2 report (:1302-1317) */
+		if (pull(k, 4, &a))
+			C_mcast_recs(k, BE16(k, a + 2));
+		break;
+	case 144: case 146: case 150: case 151:      /* :1319-1332, 1350-1353, 1405-1434 */
+		pull(k, 4, NULL);
+		break;
+	case 145:                                    /* :1334-1348 */
+		if (pull(k, 4, NULL))
+			C_addrs(k, (uint8_t)(pkt_len(k) / 16));
+		break;
+	case 149:                                    /* :1388-1403 */
+		if (pull(k, 8, NULL))
+			C_nd_ops(k);
+		break;
+	}
+}
+
 static int run_layer(P *k, int id)
 {
 	uint32_t start = k->data;
@@ -1402,9 +1746,18 @@ static int run_layer(P *k, int id)
 	case NSD_OPS_ICMPV6:         return L_icmpv6(k, start);
 	case NSD_OPS_SLL:            return L_sll(k);
 	default:
-		/* ARP, LLDP, IGMP, DCCP (and non-Ethernet heads): host-rendered leaves */
+		/* ARP, LLDP, IGMP, DCCP (and non-Ethernet heads): host-rendered
+		 * leaves, the cursor where their pulls end */
 		k->host = 1;
 		k->data = start;
+		if (id == NSD_OPS_ARP)
+			C_arp(k);
+		else if (id == NSD_OPS_LLDP)
+			C_lldp(k);
+		else if (id == NSD_OPS_IGMP)
+			C_igmp(k);
+		else if (id == NSD_OPS_DCCP)
+			C_dccp(k);
 		if (k->t)
 			k->t->unsupported = 1;
 		return 0;

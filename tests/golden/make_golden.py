@@ -5,6 +5,8 @@
   edge.pcap            tests/edge_cases.py (every §8a quirk)
   big.pcap             records longer than a batch carries (NSD_MAX_CAPLEN <
                        caplen <= read_pcap's 1 MiB buffer) between short ones
+  leaves.pcap          tests/leaf_cases.py: ARP / DCCP / IGMP / LLDP / ICMPv6
+                       130-154 frames (NORM and LESS text; --leaves-only)
   <pcap>.m<M>.w<C>.txt.gz / .ends.json
                        text printed by the REFERENCE parser objects
                        (oracle/_ref/nsref) for print mode M, terminal width C
@@ -31,6 +33,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 import edge_cases  # noqa: E402
+import leaf_cases  # noqa: E402
 import nsd_testlib as T  # noqa: E402
 
 MODES = [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX, T.PRINT_ASCII, T.PRINT_HEX_ASCII]
@@ -101,6 +104,12 @@ def big_cases():
 
 def main():
     T.build_native()
+    leaves = os.path.join(HERE, "leaves.pcap")
+    T.write_pcap(leaves, leaf_cases.cases())
+    for m in (T.PRINT_NORM, T.PRINT_LESS):
+        save_text(os.path.join(HERE, f"leaves.m{m}.w65535"), T.run_ref(leaves, mode=m, cols=65535))
+    if "--leaves-only" in sys.argv:
+        return
     big = os.path.join(HERE, "big.pcap")
     T.write_pcap(big, big_cases())
     for m in MODES:

@@ -55,6 +55,20 @@ def test_edge_cases(mode):
     _check(frames, desc, mode)
 
 
+@pytest.mark.parametrize("align", [1, 16])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_leaf_walks(mode, align):
+    """The device walks of the host-rendered leaves (nsd_leaf.h): ARP, DCCP,
+    IGMP, LLDP and ICMPv6 130-154 frames (tests/golden/leaves.pcap, whose
+    reference text pins the end cursors through the exit-op dump); every
+    record's data_off is the leaf's end, as the oracle's."""
+    _, pkts = T.read_pcap(T.GOLDEN + "/leaves.pcap")
+    frames, desc = T.batch_from_packets(pkts, align=align)
+    rec, _ = _check(frames, desc, mode)
+    host = rec["nflags"] & 0x10 != 0
+    assert host.sum() >= 2000
+
+
 @pytest.mark.parametrize("align", [1, 2, 16])
 def test_edge_cases_unaligned(align):
     frames, desc = T.batch_from_packets(edge_cases.cases(), align=align)

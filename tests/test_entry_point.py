@@ -60,6 +60,19 @@ def test_entry_point_matches_golden(harness, tmp_path, name, mode):
     assert err.count(b"Port name resolution won't be available.") == 4
 
 
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_entry_point_leaves_match_golden(harness, tmp_path, mode):
+    """ARP / DCCP / IGMP / LLDP / ICMPv6 130-154 frames (tests/leaf_cases.py):
+    the walk's leaf end (nsd_leaf.h) must agree with the renderer's pulls on
+    every layer (run_layer aborts otherwise) and the text, exit-op dump
+    included, equals the reference objects' byte for byte."""
+    gold = load_golden(f"leaves.m{mode}.w65535")
+    got, _ = run_harness(harness, os.path.join(T.GOLDEN, "leaves.pcap"), mode, tmp_path)
+    assert len(got) == len(gold)
+    bad = [i for i in range(len(gold)) if got[i] != gold[i]]
+    assert not bad, f"packets {bad[:10]} differ; first: {got[bad[0]][:400]!r} vs {gold[bad[0]][:400]!r}"
+
+
 @pytest.mark.parametrize("name", ["tiny", "edge"])
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
 def test_entry_point_wrapped_80(harness, tmp_path, name, mode):
@@ -125,6 +138,13 @@ def _assert_cpu_walk_matches_oracle(frames, desc, mode):
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX])
 def test_cpu_walk_edge_vs_oracle(mode):
     frames, desc = T.batch_from_packets(edge_cases.cases())
+    _assert_cpu_walk_matches_oracle(frames, desc, mode)
+
+
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_cpu_walk_leaves_vs_oracle(mode):
+    _, pkts = T.read_pcap(os.path.join(T.GOLDEN, "leaves.pcap"))
+    frames, desc = T.batch_from_packets(pkts)
     _assert_cpu_walk_matches_oracle(frames, desc, mode)
 
 

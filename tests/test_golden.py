@@ -93,6 +93,28 @@ def test_formatter_matches_golden(name, mode):
         assert icmpv6_bodies >= 40           # ICMPv6 130-154 bodies (nsd_format_icmpv6.h)
 
 
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_formatter_leaves_match_golden(mode):
+    """The leaf frames (tests/leaf_cases.py): the oracle's records carry each
+    leaf's end cursor (where the exit op's dump starts), the formatter checks
+    its renderer's pulls end there, and the text equals the reference's."""
+    lt, pkts, frames, desc = batch("leaves")
+    gold = load_golden(f"leaves.m{mode}.w65535")
+    rec, ext, _, _ = T.oracle_records(frames, desc, linktype=lt, mode=mode)
+    texts, rc = nsd.format_batch(frames, desc, rec, ext, mode=mode, linktype=lt)
+    host = moved = 0
+    for i in range(len(pkts)):
+        assert rc[i] == 0, f"packet {i}: status {rc[i]}"
+        assert texts[i] == gold[i], f"packet {i} differs"
+        if rec[i]["nflags"] & 0x10:
+            host += 1
+            n = int(rec[i]["nflags"]) & 7
+            start = int(rec[i]["off2"][n - 2]) * 2 if 1 < n < 7 else -1
+            moved += int(rec[i]["data_off"]) > start >= 0
+    # most leaves pull something (PRINT_LESS: no ICMPv6 bodies, IGMP pulls nothing)
+    assert host >= (2500 if mode == T.PRINT_NORM else 2000) and moved >= 1200, (host, moved)
+
+
 @pytest.mark.parametrize("name", ["tiny", "edge"])
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
 def test_wrap_matches_golden(name, mode):

@@ -162,6 +162,18 @@ def test_replay_matches_golden(tmp_path, name, mode):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_replay_leaves_match_golden(tmp_path, mode):
+    """The leaf frames end to end: device records (leaf end cursors from the
+    device walk) -> host text == the reference's."""
+    gold = TG.load_golden(f"leaves.m{mode}.w65535")
+    path, keep = replayable("leaves", mode, tmp_path)
+    n, text = nsd.replay_pcap(path, mode=mode, threads=4, cols=65535)
+    assert n == len(keep) == len(gold)
+    assert text == b"".join(gold)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
 def test_replay_wrapped_and_filtered(tmp_path, mode):
     """80-column tprintf wrap over the replay stream, and a BPF filter in
     front (only the accepted records print, in file order)."""
