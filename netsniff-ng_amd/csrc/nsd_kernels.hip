@@ -33,7 +33,7 @@ constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
 constexpr int WIN1 = 64;         // bytes per staged window, pass 1
 #ifndef NSD_WIN2
-#define NSD_WIN2 64
+#define NSD_WIN2 128
 #endif
 constexpr int WIN2 = NSD_WIN2;   // bytes per staged window, general-walk continuation
 // window row stride in dwords (odd: 64 lanes reading the same offset hit 64
@@ -71,9 +71,13 @@ struct HbmBytes {
 };
 
 // Byte source over an LDS window (aligned coordinates, see top).
-// FAST: bytes outside the window are not fetched; the source records the
-// miss and the walk gives the packet up to pass 2.  Otherwise they come from
-// HBM (zero past caplen).
+// FAST (the fast walk): the window is a zero-padded 17-dword row (bytes past
+// caplen zeroed by stage_write); bytes outside it are not fetched, the
+// source records the miss and the walk gives the packet up to the general
+// walk.  Otherwise (the general walk's continuation windows, stage_glds): a
+// row of WIN bytes filled by LDS-DMA with its 16-byte slots XOR-swizzled
+// (dword j at j ^ sw) and nothing zeroed, so every read masks the bytes at
+// offsets >= caplen itself; bytes outside the window come from HBM.
 template <bool FAST, int WIN>
 struct LSrc {
 	const uint32_t *win;     // this lane's window row
@@ -84,8 +88,9 @@ struct LSrc {
 	uint32_t m;              // off & 15
 	uint32_t wb;             // aligned position of window byte 0 (multiple of 16)
 	mutable bool miss;
+	uint32_t sw;             // continuation rows: slot swizzle (dword index xor)
 
-	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return win[j]; }
+	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return FAST ? win[j] : win[j ^ sw]; }
 	__device__ __forceinline__ int lay3(uint32_t key) const { return lay3t[key & 255]; }
 	__device__ __forceinline__ uint32_t step(int id) const { return stept[id & 31]; }
 	__device__ __forceinline__ uint32_t l2h(uint32_t h) const { return stept[32 + (h & 31)]; }
@@ -98,26 +103,33 @@ struct LSrc {
 		uint32_t j = r >> 2;
 		j = j > WIN / 4 - 1 ? WIN / 4 - 1 : j;
 		const uint32_t v = __builtin_amdgcn_alignbyte(dw(j + 1), dw(j), r & 3);
-		return o >= caplen ? 0u : v;
+		if constexpr (FAST) {
+			return o >= caplen ? 0u : v;
+		} else {
+			const uint32_t left = o >= caplen ? 0u : caplen - o;
+			return left >= 4 ? v : v & ((1u << (8 * left)) - 1u);
+		}
 	}
 	__device__ __forceinline__ bool missed() const { return miss; }
 	__device__ __forceinline__ uint8_t b(uint32_t o) const
 	{
 		const uint32_t r = o + m - wb;
-		if (r < WIN)
-			return (uint8_t)(dw(r >> 2) >> ((r & 3) * 8));
 		if constexpr (FAST) {
+			if (r < WIN)
+				return (uint8_t)(dw(r >> 2) >> ((r & 3) * 8));
 			if (o < caplen)
 				miss = true;
 			return 0;
 		} else {
-			return o < caplen ? p[o] : 0;
+			if (o >= caplen)
+				return 0;
+			return r < WIN ? (uint8_t)(dw(r >> 2) >> ((r & 3) * 8)) : p[o];
 		}
 	}
 	__device__ __forceinline__ uint16_t le16(uint32_t o) const
 	{
 		const uint32_t r = o + m - wb;
-		if (r + 1 < WIN && (r & 3) != 3)
+		if (r + 1 < WIN && (r & 3) != 3 && (FAST || o + 2 <= caplen))
 			return (uint16_t)(dw(r >> 2) >> ((r & 3) * 8));
 		return (uint16_t)(b(o) | b(o + 1) << 8);
 	}
@@ -152,7 +164,7 @@ struct LSrc {
 	// inspects from its start, c_step's `need`): general walk only
 	__device__ __forceinline__ bool near_end(uint32_t o, int id) const
 	{
-		const uint32_t need = step(id) >> 24;
+		const uint32_t need = step(id) >> 25;
 		return need && o < caplen && o + m + need > wb + WIN;
 	}
 	// sum of `nwords` little-endian u16 words from `o` (csum.h:16-17)
@@ -160,7 +172,7 @@ struct LSrc {
 	{
 		uint32_t sum = 0;
 		const uint32_t r = o + m - wb;
-		if (!(r & 1) && in_window(o, 2 * nwords)) {
+		if (!(r & 1) && in_window(o, 2 * nwords) && (FAST || o + 2 * nwords <= caplen)) {
 			uint32_t j = r >> 2, k = nwords;
 			if ((r & 2) && k) { sum += dw(j) >> 16; j++; k--; }
 			for (; k >= 2; k -= 2, j++) { const uint32_t v = dw(j); sum += (v & 0xFFFF) + (v >> 16); }
@@ -248,6 +260,42 @@ __device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks<WIN> &c
 		dst[2] = w[2];
 		dst[3] = w[3];
 	}
+}
+
+// The continuation windows (WIN bytes per lane, CPP = WIN / 16 slots) by
+// LDS-DMA: wave-instruction r's lane l fills slot l % CPP of row
+// q = r * (64 / CPP) + l / CPP (the destination is lane-linear), loading
+// chunk (l % CPP) ^ swz(q) of packet q's window, so row q holds its chunk c
+// in slot c ^ swz(q) and the lanes reading one window offset spread over
+// the banks (dword j of row q at j ^ (swz(q) << 2)).  No VGPR holds the
+// window on the way.  Chunks wholly past the frame are not loaded (the
+// source masks the bytes past caplen instead).  abase: this lane's aligned
+// window start in HBM; rem: bytes from there to the frame's aligned end (0:
+// the lane takes no window).
+__device__ __forceinline__ uint32_t swz_of(uint32_t q, int cpp) { return (q >> 1) & (uint32_t)(cpp - 1); }
+
+template <int WIN>
+__device__ __forceinline__ void stage_glds(uint32_t *wwin, uint64_t abase, uint32_t rem, int lane)
+{
+	constexpr int CPP = WIN / 16, PER = 64 / CPP;
+	static_assert(CPP * PER == 64, "a window size whose slots tile a wave");
+	const uint32_t lo = (uint32_t)abase;
+	// the high address dword (a 48-bit VA) shares its word with min(rem, 0xFFFF)
+	const uint32_t hr = (uint32_t)(abase >> 32) | (rem < 0xFFFFu ? rem : 0xFFFFu) << 16;
+#pragma unroll 2
+	for (int r = 0; r < CPP; r++) {
+		const int q = r * PER + lane / CPP;
+		const uint32_t alo = __shfl(lo, q, 64), ahr = __shfl(hr, q, 64);
+		const uint32_t c = ((uint32_t)lane % CPP) ^ swz_of((uint32_t)q, CPP);
+		if (16 * c < (ahr >> 16)) {
+			const uint64_t a = ((uint64_t)(ahr & 0xFFFFu) << 32 | alo) + 16 * c;
+			__builtin_amdgcn_global_load_lds((const void *)a,
+							 (__attribute__((address_space(3))) void *)(wwin + r * 256), 16, 0,
+							 0);
+		}
+	}
+	// the DMA's LDS writes are ordered for this wave's reads by its vmcnt only
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -373,9 +421,11 @@ __device__ __forceinline__ uint64_t pend_entry(uint32_t i, uint32_t off, uint32_
 
 // ---- the fused kernel ---------------------------------------------------------
 // Block-level shared state of one dissect launch.
-constexpr int WINMAX = WIN1 > WIN2 ? WIN1 : WIN2;
+// a wave's window area: the fast walk's 17-dword rows, then (same words) the
+// continuation's WIN2-byte rows
+constexpr int WINWORDS = 64 * row_of(WIN1) > 16 * WIN2 ? 64 * row_of(WIN1) : 16 * WIN2;
 struct Shared {
-	uint32_t win[WAVES][64 * row_of(WINMAX)];   // staged windows (fast walk, then continuations)
+	uint32_t win[WAVES][WINWORDS];              // staged windows (fast walk, then continuations)
 	unsigned long long cnt[NSD_NCOUNTERS];      // block counters
 	uint8_t lay3[256];                          // eth_lay3
 	uint32_t step[64];                          // c_step, c_lay2h (general walk)
@@ -456,14 +506,14 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 					return ((w.chain >> (5 * j)) & 31) | (uint32_t)off_of(w, j) << 16;
 				return j < nl ? g.lay[(j - NSD_REC_MAX_LAYERS) * 64 + lane] : 0u;
 			};
+			// layers 0 .. DEEP-1 (deeper ones are in the entry already)
+			constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
+			static_assert(DEEP % 4 == 0 && DEEP <= 16, "whole uint4 groups of a short entry");
 			*(uint4 *)e = make_uint4(i, nl, 0, 0);
-			*(uint4 *)(e + 4) = make_uint4(lv(0), lv(1), lv(2), lv(3));
-			if (nl > 4)
-				*(uint4 *)(e + 8) = make_uint4(lv(4), lv(5), lv(6), lv(7));
-			if (nl > 8)
-				*(uint4 *)(e + 12) = make_uint4(lv(8), lv(9), lv(10), lv(11));
-			if (nl > 12)
-				*(uint4 *)(e + 16) = make_uint4(lv(12), lv(13), lv(14), lv(15));
+#pragma unroll
+			for (uint32_t g0 = 0; g0 < DEEP; g0 += 4)
+				if (g0 == 0 || nl > g0)
+					*(uint4 *)(e + 4 + g0) = make_uint4(lv(g0), lv(g0 + 1), lv(g0 + 2), lv(g0 + 3));
 		}
 	}
 	if (fin)
@@ -490,7 +540,7 @@ __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restr
 					      const uint32_t *__restrict__ sll, uint4 *__restrict__ rec,
 					      const GenSink &g, Pending &pq, FlagCnt &fc)
 {
-	constexpr int ROW = row_of(WIN2);
+	constexpr int ROW = WIN2 / 4;
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
 	const bool on = fw != FW_DONE;
@@ -510,12 +560,13 @@ __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restr
 	bool have = on;
 	uint32_t wb = (w.data + m) & ~15u;
 	while (__ballot(have)) {
-		Chunks<WIN2> cc;
-		stage_load<true, WIN2>(cc, frames, d, wb | (have ? 0u : 0x80000000u), lane);
-		stage_write(&sh.win[wv][0], cc, lane);
-		wave_sync_lds();
+		// (the window's address and extent are recomputed per round from the
+		// descriptor rather than kept live across the walk: registers)
+		const uint32_t lim = caplen + m;   // first aligned position past the frame
+		stage_glds<WIN2>(&sh.win[wv][0], (uint64_t)(frames + (NSD_DESC_OFF(d) & ~15ull)) + wb,
+				 have && wb < lim ? lim - wb : 0u, lane);
 		const LSrc<false, WIN2> src{ &sh.win[wv][lane * ROW], sh.lay3, sh.step, frames + NSD_DESC_OFF(d),
-					     caplen, m, wb, false };
+					     caplen, m, wb, false, swz_of((uint32_t)lane, WIN2 / 16) << 2 };
 		bool susp;
 		for (;;) {
 			const bool run = have && w.id != 0;

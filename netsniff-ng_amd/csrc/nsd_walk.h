@@ -88,7 +88,7 @@ struct WalkOut {
 // packet's pool entry when its walk ends), deeper layers straight into the
 // packet's pool entry (taken when the chain reaches that depth).  Pool words
 // come from per-wave chunks (ext_take).
-#define NSD_LDS_LAYERS 10
+#define NSD_LDS_LAYERS 6
 struct GenSink {
 	uint32_t *pool;               // the ext pool
 	uint32_t pool_words;
@@ -166,9 +166,10 @@ __device__ __forceinline__ void GenSink::layer(const WalkOut &w, uint32_t k, int
 
 __device__ __forceinline__ void GenSink::take_deep(bool deep_first, WalkOut &w) const
 {
-	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
 	if (__ballot(deep_first)) {
-		const uint32_t sb = ext_take(*this, deep_first, NSD_EXT_WORDS(DEEP + 1));
+		// room for every layer the record may hold (the chain's length is not
+		// known yet)
+		const uint32_t sb = ext_take(*this, deep_first, NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS));
 		if (deep_first) {
 			w.slot = sb;
 			w.ext_on = true;

@@ -101,6 +101,86 @@ def test_block_sll_copied():
     assert set(sll["protocol"]) == {0x0800} and set(sll["hatype"]) == {1} and set(sll["family"]) == {17}
 
 
+def _live_ring():
+    import ring_live as RL
+    r = RL.open_ring()
+    if r is None:
+        pytest.skip("AF_PACKET sockets need CAP_NET_RAW here")
+    return r
+
+
+def _live_frames():
+    """Edge and leaf frames for the loopback ring, minus 802.1Q / 802.1ad ones
+    (the receive path moves their tag into tp_vlan_tci) and jumbo ones."""
+    import leaf_cases
+    import ring_live as RL
+    pkts = [p for p in edge_cases.cases() + leaf_cases.cases(300, seed=5) if 14 <= len(p) <= 9000]
+    return RL.marked([p for p in pkts if p[12:14] not in (b"\x81\x00", b"\x88\xa8")])
+
+
+def test_live_ring_block_desc():
+    """A real PACKET_RX_RING on lo (ring_rx.c:28-229 setup): the frames the
+    retired blocks hold, through nsd_t3_block_desc with netsniff-ng's skip
+    rule for loopback's outgoing copies (skip_packet, netsniff-ng.c), are
+    the frames sent, in order."""
+    import ring_live as RL
+    r = _live_ring()
+    try:
+        pkts = _live_frames()
+        r.send(pkts)
+
+        def frames_of(k):
+            blk = r.block(k)
+            desc = nsd.t3_block_desc(blk, packet_type=-1, lo_ifindex=r.ifindex)
+            return [bytes(blk[int(d) & 0xFFFFFFFFFF:][:int(d) >> 40]) for d in desc]
+        got = RL.collect(r, len(pkts), frames_of)
+        assert got == pkts
+    finally:
+        r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_live_ring_registered_through_pipe(mode):
+    """The same ring on the GPU: each retired block is registered with
+    nsd_host_register (hipHostRegister of the mmap'd ring memory), walked
+    through nsd_pipe_submit straight from the block, and its records and
+    counters equal the oracle's."""
+    import ring_live as RL
+    from test_device_parity import assert_same_records
+    r = _live_ring()
+    pipe = nsd.Pipe(1 << 16, r.block_size, ext_words=nsd.ext_pool_words(1 << 16), depth=2, mode=mode)
+    L = nsd.lib()
+    try:
+        pkts = _live_frames()
+        r.send(pkts)
+
+        def walk(k):
+            blk = r.block(k)
+            assert L.nsd_host_register(blk.ctypes.data, blk.nbytes) == 0
+            try:
+                desc = nsd.t3_block_desc(blk, packet_type=-1, lo_ifindex=r.ifindex)
+                n = len(desc)
+                rec = np.zeros(n, dtype=nsd.REC_DTYPE)
+                ext = np.zeros(pipe.ext_words, dtype=np.uint32)
+                used = np.zeros(1, dtype=np.uint32)
+                cnt = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
+                st = np.full(1, -99, dtype=np.int32)
+                pipe.submit(blk, desc, rec, ext, used, cnt, st)
+                assert pipe.drain() == 0 and st[0] == 0
+                orec, oext, ocnt, _ = T.oracle_records(blk, desc, mode=mode)
+                assert_same_records(rec, orec, ext[:int(used[0])], oext)
+                assert np.array_equal(cnt, ocnt)
+                return [bytes(blk[int(d) & 0xFFFFFFFFFF:][:int(d) >> 40]) for d in desc]
+            finally:
+                assert L.nsd_host_unregister(blk.ctypes.data) == 0
+        got = RL.collect(r, len(pkts), walk)
+        assert got == pkts
+    finally:
+        pipe.close()
+        r.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
 def test_cooked_ring_through_pipe(mode):
