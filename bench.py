@@ -3,7 +3,11 @@
 Workload (BASELINE.json configs[1], "C2"): 16,777,216 synthetic 64 B
 Eth/IPv4/UDP frames per GPU, resident in HBM; one step = one pass of the
 dissector chain kernel over the batch (records + ext + per-protocol counters)
-plus, for N > 1 GPUs, the RCCL all-reduce of the counter vector.
+plus, for N > 1 GPUs, the RCCL all-reduce of the counter vector.  Records
+are the compact 8-byte form by default (nsd_crec: ops ids, IPv4 checksum,
+flags; the renderer re-derives the cursors), --records full
+times the 16-byte nsd_rec; the other form is measured beside it
+("other_records").
 --config imix / ipv6x select C3 / C4 as the headline instead; --shards S
 walks S contiguous 16M shards of the same stream as one batch on one GPU
 (--config imix --shards 8 = C5's 128M packets on a single MI355X).
@@ -52,7 +56,8 @@ CONFIGS = {
 }
 LEGS = ("imix", "ipv6x")
 HBM_PEAK_GBS = 8000.0      # MI355X spec (MI355X_MICROARCH.md)
-REC_B, DESC_B = 16, 8
+REC_B, DESC_B = 16, 8          # record bytes of the 16-byte form, descriptor bytes
+CREC_B = 8                     # compact record (nsd_crec)
 MODES = ["PRINT_NORM", "PRINT_LESS", "PRINT_HEX", "PRINT_ASCII", "PRINT_HEX_ASCII", "PRINT_NONE"]
 
 
@@ -96,8 +101,10 @@ def library_info():
 class Batch:
     """A config's packets resident in HBM plus the output buffers of one walk."""
 
-    def __init__(self, key, n, lo, shards, dev):
+    def __init__(self, key, n, lo, shards, dev, compact=True):
         self.key, self.n_shard, self.shards = key, n, shards
+        self.compact = compact
+        self.rec_b = CREC_B if compact else REC_B
         self.n = n * shards
         cfg = CONFIGS[key]["cfg"]
         self.frames, self.desc, desc_np = T.make_device_batch(cfg, self.n, lo=lo, device=dev)
@@ -106,7 +113,7 @@ class Batch:
         self.line_bytes = int(np.minimum(caps, 64).sum())   # first 64-B line per frame (BPF leg)
         del desc_np
         ext_w = nsd.ext_pool_words(self.n) if key == "ipv6x" else nsd.ext_pool_words(self.n // 64)
-        self.rec = torch.empty(self.n * REC_B, dtype=torch.uint8, device=dev)
+        self.rec = torch.empty(self.n * self.rec_b, dtype=torch.uint8, device=dev)
         self.ext = torch.empty(ext_w, dtype=torch.int32, device=dev)
         self.ext_used = torch.zeros(1, dtype=torch.int32, device=dev)
         self.counters = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device=dev)
@@ -118,8 +125,13 @@ class Batch:
         self.counters.zero_()
         if ev is not None:
             ev[0].record()
-        nsd.dissect_device(self.frames, self.desc, mode=mode, rec=self.rec, ext=self.ext,
-                           ext_used=self.ext_used, counters=self.counters, grid=grid, workspace=self.ws)
+        if self.compact:
+            assert not grid, "--grid applies to the 16-byte record kernels"
+            nsd.dissect_device_compact(self.frames, self.desc, mode=mode, crec=self.rec, ext=self.ext,
+                                       ext_used=self.ext_used, counters=self.counters, workspace=self.ws)
+        else:
+            nsd.dissect_device(self.frames, self.desc, mode=mode, rec=self.rec, ext=self.ext,
+                               ext_used=self.ext_used, counters=self.counters, grid=grid, workspace=self.ws)
         if ev is not None:
             ev[1].record()
 
@@ -127,13 +139,13 @@ class Batch:
         if self.wsum is None:
             return None
         read_b = DESC_B * self.n + self.wsum
-        total_b = read_b + REC_B * self.n
+        total_b = read_b + self.rec_b * self.n
         achieved = total_b / (kern_ms * 1e-3) / 1e9
         r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(achieved / HBM_PEAK_GBS, 4),
              "traffic": None if traffic is None else round(traffic["bytes_per_launch"]),
              "read_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-             "bytes_per_pkt": {"read": round(read_b / self.n, 2), "write": REC_B},
+             "bytes_per_pkt": {"read": round(read_b / self.n, 2), "write": self.rec_b},
              "kernel_ms": round(kern_ms, 4)}
         if traffic is not None:
             r["traffic_bytes_per_pkt"] = {"read": round(traffic["read_bytes"] / self.n, 1),
@@ -166,7 +178,7 @@ def pmc_child(args):
     torch.cuda.set_device(0)
     for key in args.pmc_configs.split(","):
         shards = args.shards if key == args.config else 1
-        b = Batch(key, args.packets, 0, shards, torch.device("cuda", 0))
+        b = Batch(key, args.packets, 0, shards, torch.device("cuda", 0), compact=args.records == "compact")
         for _ in range(args.steps):
             b.step(args.mode, args.grid)
         torch.cuda.synchronize()
@@ -188,7 +200,7 @@ def pmc_traffic(args, keys, steps=3):
                    "run", "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__),
                    "--pmc-child", "--pmc-configs", ",".join(keys), "--config", args.config,
                    "--packets", str(args.packets), "--shards", str(args.shards), "--steps", str(steps),
-                   "--mode", str(args.mode), "--grid", str(args.grid)]
+                   "--mode", str(args.mode), "--grid", str(args.grid), "--records", args.records]
             r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if r.returncode != 0 or not files:
@@ -422,6 +434,8 @@ def main():
     ap.add_argument("--shards", type=int, default=1, help="contiguous shards walked as one batch per GPU")
     ap.add_argument("--mode", type=int, default=nsd.PRINT_NORM)
     ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--records", default="compact", choices=["compact", "full"],
+                    help="record form of the timed launches: 8-byte nsd_crec or 16-byte nsd_rec")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=16.0, help="CPU baseline duration (4 legs)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end pass")
@@ -462,7 +476,8 @@ def main():
 
     n = args.packets
     lo = rank * n * args.shards
-    b = Batch(args.config, n, lo, args.shards, dev)
+    compact = args.records == "compact"
+    b = Batch(args.config, n, lo, args.shards, dev, compact=compact)
 
     for _ in range(args.warmup):
         b.step(args.mode, args.grid)
@@ -504,9 +519,20 @@ def main():
     b.free()
     torch.cuda.empty_cache()
 
+    # the other record form over the same workload (kernel time, roofline)
+    other = None
+    if solo and not args.no_legs:
+        ob = Batch(args.config, n, lo, args.shards, dev, compact=not compact)
+        oms = time_steps(ob, args.mode, args.steps, args.warmup, 0)
+        other = {"records": "full 16 B (nsd_rec)" if compact else "compact 8 B (nsd_crec)",
+                 "value": round(ob.n / (oms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
+                 "roofline": ob.roofline(oms, None, copy_gbs)}
+        ob.free()
+        torch.cuda.empty_cache()
+
     leg_out = {}
     for key in legs:
-        lb = Batch(key, n, 0, 1, dev)
+        lb = Batch(key, n, 0, 1, dev, compact=compact)
         ms = time_steps(lb, args.mode, args.steps, args.warmup, args.grid)
         lc = lb.counters.cpu().numpy().view(np.uint64)
         assert int(lc[nsd.CNT_PKTS]) == lb.n, f"{key}: counter check failed"
@@ -539,10 +565,12 @@ def main():
             "data": "synthetic (seeded splitmix64 generators, tools/nsd_synth.c)",
             "config": {"workload": workload_name(args.config, n, args.shards), "packets_per_gpu": b.n,
                        "frame_bytes_per_gpu": frame_bytes, "mode": MODES[args.mode],
+                       "records": "compact 8 B (nsd_crec)" if compact else "full 16 B (nsd_rec)",
                        "parallelism": f"dp{world}"},
             "gbps_frames": round(frame_bytes * world * args.steps / elapsed / 1e9, 1),
             "roofline": roofline,
             "legs": leg_out or None,
+            "other_records": other,
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "replay": replay,

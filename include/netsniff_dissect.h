@@ -386,6 +386,40 @@ int nsd_walk_packet_cpu(const uint8_t *pkt, uint32_t caplen, int linktype, int m
 			const nsd_sll_t *sll, nsd_rec *rec, uint32_t *ext, uint32_t ext_words,
 			uint64_t *counters);
 
+/* ---- compact records (8 bytes per packet) ---------------------------------
+ * The walk's results without the cursors: the ops ids, the IPv4 header
+ * checksum and the flags, but no layer offsets, final data / tail cursor.
+ * A renderer re-derives each of those from the bytes as it prints the
+ * layer (every proto_*.c print pulls its own header), so a consumer that
+ * renders, as the reference does for every packet, loses nothing; the
+ * 16-byte nsd_rec additionally lets it cross-check the device's cursors.
+ * Layout: chain = the ops ids as in nsd_rec (5 bits each, layer count in
+ * nflags & 7), or, when (nflags & 7) == NSD_N_EXT, the ext pool slot of the
+ * chain (0xFFFFFFFF with NSD_F_OVERFLOW: pool full / chain too long); the
+ * ext entry keeps its layer offsets.  nflags, ip_csum: as in nsd_rec.  */
+typedef struct nsd_crec {
+	uint32_t chain;
+	uint16_t ip_csum;
+	uint8_t  nflags;
+	uint8_t  rsvd;
+} nsd_crec;
+
+/* nsd_dissect_device_ws / _sll writing n compact records; d_sll as in
+ * nsd_dissect_device_sll (NULL: zeros), d_workspace of nsd_workspace_bytes(n) */
+int nsd_dissect_device_compact(const uint8_t *d_frames, const nsd_desc_t *d_desc,
+			       const nsd_sll_t *d_sll, uint32_t n, int linktype, int mode,
+			       nsd_crec *d_crec, uint32_t *d_ext, uint32_t ext_words,
+			       uint32_t *d_ext_used, uint64_t *d_counters, void *d_workspace,
+			       void *stream);
+/* nsd_format_batch_sll over compact records: each layer starts where the
+ * previous one's print left the cursor; an ext chain is also checked
+ * against its entry's offsets.  A record without its chain (NSD_F_OVERFLOW)
+ * gets rc NSD_ERR_FORMAT (render it per packet: dissector_entry_point). */
+long nsd_format_batch_compact(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+			      uint32_t n, int linktype, int mode, const nsd_crec *crec,
+			      const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends,
+			      int8_t *rc);
+
 /* ---- pcap replay front end (`netsniff-ng --in f.pcap`, read_pcap
  * netsniff-ng.c:640-770; pcap_io.h / pcap_sg.c record formats) ---------------
  * nsd_pcap_open: validates the file header (tcpdump usec / nsec, Kuznetzov,

@@ -989,80 +989,63 @@ void render_ascii(std::string &s, const uint8_t *pkt, uint32_t caplen, uint32_t 
 	dump_ascii(o, Frame{ pkt, caplen }, from, len);
 }
 
-// Render one packet; returns NSD_OK or NSD_ERR_FORMAT (text so far kept).
-int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-		  const nsd_rec &rec, const uint32_t *ext_pool, const nsd_sll_t *sll)
+// PRINT_HEX / _ASCII / _HEX_ASCII: every process() is NULL (dissector.c:26-38,
+// 108-118); true when `mode` is one of those (or PRINT_NONE) and was handled
+static bool format_no_chain(Out &o, const Frame &f, uint32_t caplen, int mode)
 {
-	Out o(s);
-	Frame f{ pkt, caplen };
-
 	if (mode == PRINT_NONE)
-		return NSD_OK;
-	if (mode != PRINT_NORM && mode != PRINT_LESS) {
-		// every process() is NULL in these modes (dissector.c:26-38, 108-118)
-		if (mode == PRINT_HEX) {
-			if (caplen) { dump_hex(o, f, 0, caplen); o << "\n"; }
-		} else if (mode == PRINT_ASCII) {
-			if (caplen) { dump_ascii(o, f, 0, caplen); o << "\n"; }
-		} else {
-			if (caplen) { dump_ascii(o, f, 0, caplen); dump_hex(o, f, 0, caplen); }
-			o << "\n";
-		}
-		return NSD_OK;
-	}
-
-	// the chain as the device recorded it
-	uint32_t n = rec.nflags & 7u;
-	uint8_t ids[NSD_EXT_MAX_LAYERS];
-	uint16_t offs[NSD_EXT_MAX_LAYERS];
-	if (n == NSD_N_EXT) {
-		uint32_t slot;
-		memcpy(&slot, rec.off2, 4);
-		if (!ext_pool || slot == 0xFFFFFFFFu || (rec.nflags & NSD_F_OVERFLOW))
-			return NSD_ERR_FORMAT;
-		n = NSD_EXT_NLAYERS(ext_pool, slot);
-		if (n > NSD_EXT_MAX_LAYERS)
-			return NSD_ERR_FORMAT;
-		for (uint32_t k = 0; k < n; k++) {
-			ids[k] = (uint8_t)NSD_EXT_ID(ext_pool, slot, k);
-			offs[k] = (uint16_t)NSD_EXT_OFF(ext_pool, slot, k);
-		}
+		return true;
+	if (mode == PRINT_NORM || mode == PRINT_LESS)
+		return false;
+	if (mode == PRINT_HEX) {
+		if (caplen) { dump_hex(o, f, 0, caplen); o << "\n"; }
+	} else if (mode == PRINT_ASCII) {
+		if (caplen) { dump_ascii(o, f, 0, caplen); o << "\n"; }
 	} else {
-		for (uint32_t k = 0; k < n; k++) {
-			ids[k] = (uint8_t)((rec.chain >> (5 * k)) & 31);
-			offs[k] = k ? (uint16_t)(rec.off2[k - 1] * 2u) : 0;
-		}
+		if (caplen) { dump_ascii(o, f, 0, caplen); dump_hex(o, f, 0, caplen); }
+		o << "\n";
 	}
-	const bool host = rec.nflags & NSD_F_HOST;
+	return true;
+}
+
+// The chain's text: layers ids[0..n) as dissector_main runs them, then the
+// exit op.  offs: the layer starts the walk recorded (each layer's print must
+// end exactly where the next one starts), or NULL: each layer starts where
+// the previous print left the cursor (compact records).  end: the walk's
+// final {data, tail} to check, or NULL.
+static int format_chain(Out &o, const Frame &f, int linktype, int mode, uint32_t n, const uint8_t *ids,
+			const uint16_t *offs, const uint32_t *end, uint16_t ip_csum, uint8_t nflags,
+			const nsd_sll_t *sll)
+{
+	const bool host = nflags & NSD_F_HOST;
 	if (n == 0 && is_lt(linktype, NSD_LINKTYPE_EN10MB))
 		return NSD_ERR_FORMAT;
-
-	uint32_t tail = caplen, data = rec.data_off;
+	if (host && n == 0)
+		return NSD_ERR_FORMAT;
+	uint32_t tail = f.caplen, data = 0;
 	for (uint32_t k = 0; k < n; k++) {
-		Layer L{ ids[k], offs[k], tail };
+		Layer L{ ids[k], offs ? offs[k] : data, tail };
 		if (L.start > tail)
 			return NSD_ERR_FORMAT;
-		const Done dn = render_one(o, f, L, mode, rec.ip_csum, rec.nflags & NSD_F_ICMP_BAD, sll);
+		const Done dn = render_one(o, f, L, mode, ip_csum, nflags & NSD_F_ICMP_BAD, sll);
 		if (!dn.ok)
 			return NSD_ERR_FORMAT;
-		// consistency with the record: next layer's start / final cursor
+		// consistency with the walk: the chain goes on exactly while it has
+		// layers, and (16-byte records, ext entries) ends where it recorded
 		// (for a host-rendered leaf too: the walk kept where its pulls end)
 		if (k + 1 < n) {
-			if (!dn.next || dn.data != offs[k + 1])
+			if (!dn.next || (offs && dn.data != offs[k + 1]))
 				return NSD_ERR_FORMAT;
 		} else {
-			if (dn.next || dn.data != rec.data_off || dn.tail != rec.tail_off)
+			if (dn.next || (end && (dn.data != end[0] || dn.tail != end[1])))
 				return NSD_ERR_FORMAT;
 		}
 		tail = dn.tail;
 		data = dn.data;
 	}
-	if (host && n == 0)
-		return NSD_ERR_FORMAT;
-
 	// exit op (dissector.c:60-61) over what the last layer left
 	if (mode == PRINT_NORM) {
-		const uint32_t len = rec.tail_off - data;
+		const uint32_t len = tail - data;
 		if (len) {
 			dump_ascii(o, f, data, len);
 			dump_hex(o, f, data, len);
@@ -1070,6 +1053,70 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 	}
 	o << "\n";
 	return NSD_OK;
+}
+
+// the ext entry's chain (NSD_ERR_FORMAT when there is none)
+static int ext_chain(const uint32_t *ext_pool, uint32_t slot, uint8_t nflags, uint32_t &n, uint8_t *ids,
+		     uint16_t *offs)
+{
+	if (!ext_pool || slot == 0xFFFFFFFFu || (nflags & NSD_F_OVERFLOW))
+		return NSD_ERR_FORMAT;
+	n = NSD_EXT_NLAYERS(ext_pool, slot);
+	if (n > NSD_EXT_MAX_LAYERS)
+		return NSD_ERR_FORMAT;
+	for (uint32_t k = 0; k < n; k++) {
+		ids[k] = (uint8_t)NSD_EXT_ID(ext_pool, slot, k);
+		offs[k] = (uint16_t)NSD_EXT_OFF(ext_pool, slot, k);
+	}
+	return NSD_OK;
+}
+
+// Render one packet; returns NSD_OK or NSD_ERR_FORMAT (text so far kept).
+int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+		  const nsd_rec &rec, const uint32_t *ext_pool, const nsd_sll_t *sll)
+{
+	Out o(s);
+	Frame f{ pkt, caplen };
+	if (format_no_chain(o, f, caplen, mode))
+		return NSD_OK;
+	// the chain as the device recorded it
+	uint32_t n = rec.nflags & 7u;
+	uint8_t ids[NSD_EXT_MAX_LAYERS];
+	uint16_t offs[NSD_EXT_MAX_LAYERS];
+	if (n == NSD_N_EXT) {
+		uint32_t slot;
+		memcpy(&slot, rec.off2, 4);
+		if (ext_chain(ext_pool, slot, rec.nflags, n, ids, offs) != NSD_OK)
+			return NSD_ERR_FORMAT;
+	} else {
+		for (uint32_t k = 0; k < n; k++) {
+			ids[k] = (uint8_t)((rec.chain >> (5 * k)) & 31);
+			offs[k] = k ? (uint16_t)(rec.off2[k - 1] * 2u) : 0;
+		}
+	}
+	const uint32_t end[2] = { rec.data_off, rec.tail_off };
+	return format_chain(o, f, linktype, mode, n, ids, offs, end, rec.ip_csum, rec.nflags, sll);
+}
+
+// the same over a compact record: the layer starts come from the prints
+int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+			  const nsd_crec &rec, const uint32_t *ext_pool, const nsd_sll_t *sll)
+{
+	Out o(s);
+	Frame f{ pkt, caplen };
+	if (format_no_chain(o, f, caplen, mode))
+		return NSD_OK;
+	uint32_t n = rec.nflags & 7u;
+	uint8_t ids[NSD_EXT_MAX_LAYERS];
+	uint16_t offs[NSD_EXT_MAX_LAYERS];
+	if (n == NSD_N_EXT) {
+		if (ext_chain(ext_pool, rec.chain, rec.nflags, n, ids, offs) != NSD_OK)
+			return NSD_ERR_FORMAT;
+		return format_chain(o, f, linktype, mode, n, ids, offs, nullptr, rec.ip_csum, rec.nflags, sll);
+	}
+	for (uint32_t k = 0; k < n; k++)
+		ids[k] = (uint8_t)((rec.chain >> (5 * k)) & 31);
+	return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll);
 }
 
 // hex() / ascii() / hex_ascii() over [from, to) (proto_none.c:28-72)
@@ -1145,6 +1192,30 @@ extern "C" long nsd_format_batch_sll(const uint8_t *frames, const nsd_desc_t *de
 		const uint64_t d = desc[i];
 		int r = nsd::format_packet(s, frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), linktype,
 					   mode, rec[i], ext_pool, sll ? sll + i : nullptr);
+		if (rc)
+			rc[i] = (int8_t)r;
+		if (ends)
+			ends[i] = s.size();
+	}
+	if (s.size() > cap)
+		return -(long)s.size();
+	memcpy(out, s.data(), s.size());
+	return (long)s.size();
+}
+
+extern "C" long nsd_format_batch_compact(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+					 uint32_t n, int linktype, int mode, const nsd_crec *crec,
+					 const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends,
+					 int8_t *rc)
+{
+	if (n && (!frames || !desc || !crec))
+		return NSD_ERR_ARG;
+	std::string s;
+	s.reserve(cap ? cap : 4096);
+	for (uint32_t i = 0; i < n; i++) {
+		const uint64_t d = desc[i];
+		int r = nsd::format_packet_compact(s, frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), linktype, mode,
+						   crec[i], ext_pool, sll ? sll + i : nullptr);
 		if (rc)
 			rc[i] = (int8_t)r;
 		if (ends)

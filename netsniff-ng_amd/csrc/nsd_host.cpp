@@ -24,6 +24,10 @@ extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_des
 				  int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
 				  uint32_t ext_cap, uint32_t *d_ext_count, uint64_t *d_counters,
 				  void *d_ws, int grid, hipStream_t stream);
+extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
+				      uint32_t n, int start_id, int mode, void *d_rec, int compact, uint32_t *d_ext,
+				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters, void *d_ws,
+				      int grid, hipStream_t stream);
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
 
 // ---- device context ----------------------------------------------------
@@ -190,6 +194,23 @@ extern "C" int nsd_dissect_device_sll(const uint8_t *d_frames, const nsd_desc_t 
 		return rc ? rc : NSD_ERR_ARG;
 	rc = nsd_launch_dissect_sll(d_frames, d_desc, d_sll, n, start_for(linktype), mode, d_rec, d_ext,
 				    ext_cap, d_ext_count, d_counters, d_workspace, 0, (hipStream_t)stream);
+	return rc ? NSD_ERR_HIP : NSD_OK;
+}
+
+extern "C" int nsd_dissect_device_compact(const uint8_t *d_frames, const nsd_desc_t *d_desc,
+					  const nsd_sll_t *d_sll, uint32_t n, int linktype, int mode,
+					  nsd_crec *d_crec, uint32_t *d_ext, uint32_t ext_words,
+					  uint32_t *d_ext_used, uint64_t *d_counters, void *d_workspace,
+					  void *stream)
+{
+	if (n == 0)
+		return NSD_OK;
+	int rc = check_device_args(d_frames, d_desc, (const nsd_rec *)d_crec, d_ext, ext_words, d_ext_used,
+				   d_counters, mode);
+	if (rc || !d_workspace)
+		return rc ? rc : NSD_ERR_ARG;
+	rc = nsd_launch_dissect_rec(d_frames, d_desc, d_sll, n, start_for(linktype), mode, d_crec, 1, d_ext,
+				    ext_words, d_ext_used, d_counters, d_workspace, 0, (hipStream_t)stream);
 	return rc ? NSD_ERR_HIP : NSD_OK;
 }
 

@@ -352,10 +352,33 @@ __device__ __forceinline__ uint16_t csum_final(uint32_t sum)
 // later kernel), measured 6 % faster than a plain store in the pass-1 access
 // shape (tools/bw: 72 B read + 16 B written per packet).
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void store_rec(uint4 *rec, uint32_t i, uint4 r)
 {
 	const v4u v = { r.x, r.y, r.z, r.w };
 	__builtin_nontemporal_store(v, (v4u *)(rec + i));
+}
+
+// The record of packet i in the launch's record form: the 16-byte nsd_rec,
+// or (CR) the 8-byte nsd_crec {chain or ext slot, ip_csum, nflags} - the
+// same results without the cursors a renderer re-derives from the bytes
+template <bool CR>
+__device__ __forceinline__ void put_rec(void *rec, uint32_t i, const WalkOut &w)
+{
+	if constexpr (CR) {
+		const uint32_t nf = (w.need_ext ? NSD_N_EXT : w.n) | w.flags;
+		const v2u v = { w.need_ext ? (w.ext_on ? w.slot : 0xFFFFFFFFu) : w.chain, w.ip_csum | nf << 16 };
+		__builtin_nontemporal_store(v, (v2u *)rec + i);
+	} else {
+		store_rec((uint4 *)rec, i, pack_record(w));
+	}
+}
+
+// byte offset of packet i's nflags in the record array
+template <bool CR>
+__device__ __forceinline__ size_t nflags_at(uint32_t i)
+{
+	return CR ? (size_t)i * 8 + 6 : (size_t)i * 16 + 10;
 }
 
 // Per-wave flag counters: wave-uniform (ballot + popcount, scalar registers);
@@ -470,11 +493,12 @@ __device__ __forceinline__ uint64_t leaf_entry(uint32_t i, uint32_t start, int i
 // wave's pending list, an ext chain to the pool (layers 0..5 from the record
 // registers, 6..15 from the wave's LDS list, deeper ones already in the
 // entry), then the record and the flag counts.
-template <int MODE>
+template <int MODE, bool CR>
 __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, uint32_t caplen, const GenSink &g,
-					     uint4 *__restrict__ rec, Pending &pq, FlagCnt &fc, int lane)
+					     void *__restrict__ rec, Pending &pq, FlagCnt &fc, int lane)
 {
-	const bool lf = fin && w.leaf != 0;
+	// (the compact record has no cursor for the leaf pass to set)
+	const bool lf = !CR && fin && w.leaf != 0;
 	const uint64_t lm = __ballot(lf);
 	if (lf)
 		pq.wq[pq.wcap - 1 - (pq.nleaf + lanes_below(lm))] = leaf_entry(i, w.data, w.leaf);
@@ -517,7 +541,7 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 		}
 	}
 	if (fin)
-		store_rec(rec, i, pack_record(w));
+		put_rec<CR>(rec, i, w);
 	fc.add(w, caplen, fin);
 }
 
@@ -534,10 +558,10 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 // packets (the lines were evicted by then), per-step loads straight from
 // L2 (64 lines per wave instruction: the vector-memory address path, not the
 // bytes, bound it).
-template <int MODE>
+template <int MODE, bool CR>
 __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restrict__ frames, uint64_t d,
 					      uint32_t i, uint32_t fw, WalkOut &w, int start_id,
-					      const uint32_t *__restrict__ sll, uint4 *__restrict__ rec,
+					      const uint32_t *__restrict__ sll, void *__restrict__ rec,
 					      const GenSink &g, Pending &pq, FlagCnt &fc)
 {
 	constexpr int ROW = WIN2 / 4;
@@ -577,7 +601,7 @@ __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restr
 			gen_step<MODE>(src, act, w, g);
 		}
 		wave_sync_lds();
-		emit_general<MODE>(have && !susp, w, i, caplen, g, rec, pq, fc, lane);
+		emit_general<MODE, CR>(have && !susp, w, i, caplen, g, rec, pq, fc, lane);
 		have = have && susp;
 		if (susp)
 			wb = (w.data + m) & ~15u;
@@ -589,10 +613,10 @@ __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restr
 // the fast walk over each packet's first 64 bytes, then the general walk
 // for the lanes it could not finish (continue_walk); ICMPv4 messages past
 // the windows and host-rendered leaves go to the wave's pending list (pq).
-template <int MODE>
+template <int MODE, bool CR>
 __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict__ frames,
 					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
-					   uint4 *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
+					   void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 					   uint32_t *__restrict__ ext_used, uint32_t chunk,
 					   const uint32_t *__restrict__ sll, Pending &pq)
 {
@@ -616,7 +640,10 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			fc.pkts += FlagCnt::pc(i < n);
 			if (i < n) {
 				const uint32_t caplen = NSD_DESC_CAPLEN(desc[i]);
-				store_rec(rec, i, make_uint4(0, caplen << 16, 0, 0));
+				if constexpr (CR)
+					__builtin_nontemporal_store(v2u{ 0u, 0u }, (v2u *)rec + i);
+				else
+					store_rec((uint4 *)rec, i, make_uint4(0, caplen << 16, 0, 0));
 				fc.bytes += caplen;
 			}
 		}
@@ -690,10 +717,10 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			}
 		}
 		if (done)
-			store_rec(rec, i, pack_record(w));
+			put_rec<CR>(rec, i, w);
 		fc.add(w, caplen, done);
 		if (__ballot(deferred))
-			continue_walk<MODE>(sh, frames, d0, i, fw, w, start_id, sll, rec, g, pq, fc);
+			continue_walk<MODE, CR>(sh, frames, d0, i, fw, w, start_id, sll, rec, g, pq, fc);
 		d0 = d1;
 		d1 = d2;
 	}
@@ -709,9 +736,9 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 // them in flight per lane; sub-lanes 0 and 1 also take the message's first
 // and last chunk with the bytes outside the message masked.  A message then
 // costs a few wave instructions per KiB instead of one wave per message.
-template <int U>
+template <int U, bool CR>
 __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict__ frames,
-					  const uint64_t *__restrict__ desc, uint4 *__restrict__ rec,
+					  const uint64_t *__restrict__ desc, void *__restrict__ rec,
 					  const uint64_t *__restrict__ pend, uint32_t region)
 {
 	const int lane = threadIdx.x & 63;
@@ -765,7 +792,7 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 				const uint32_t mi = __shfl(i, src, 64);
 				const bool isbad = mon && sub == 0 && csum_final(sum) != 0;
 				if (isbad) {
-					uint8_t *nf = (uint8_t *)rec + (size_t)mi * 16 + 10;
+					uint8_t *nf = (uint8_t *)rec + nflags_at<CR>(mi);
 					*nf = *nf | NSD_F_ICMP_BAD;
 				}
 				bad += FlagCnt::pc(isbad);
@@ -808,10 +835,10 @@ __device__ __forceinline__ void leaf_pass(const uint8_t *__restrict__ frames, co
 // left pending, then sums the ICMPv4 messages they left pending; a later
 // phase reads only what the same block wrote (its pending lists), so the
 // phases need a block barrier, not a grid-wide one.
-template <int MODE>
+template <int MODE, bool CR>
 __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
-	uint4 *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
+	void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
 	uint64_t *__restrict__ pend, uint32_t region, const uint32_t *__restrict__ sll)
 {
@@ -825,14 +852,14 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	// this wave's pending list (a wave visits region / WAVES packets)
 	Pending pq{ pend + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (region / WAVES), region / WAVES, 0,
 		    0 };
-	walk_tiles<MODE>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq);
-	if (MODE == PRINT_NORM || MODE == PRINT_LESS)
-		leaf_pass<MODE>(frames, desc, rec, pq);
+	walk_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq);
+	if (!CR && (MODE == PRINT_NORM || MODE == PRINT_LESS))
+		leaf_pass<MODE>(frames, desc, (uint4 *)rec, pq);
 	if ((threadIdx.x & 63) == 0)
 		sh.pcnt[threadIdx.x >> 6] = pq.npend;
 	if (MODE == PRINT_NORM) {
 		__syncthreads();   // records final, pending lists and counts complete
-		icmp_pass<NSD_CSUM_U>(sh, frames, desc, rec, pend, region);
+		icmp_pass<NSD_CSUM_U, CR>(sh, frames, desc, rec, pend, region);
 	}
 	block_flush(sh.cnt, counters);
 }
@@ -863,28 +890,44 @@ extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 	return 8 * region_slots(n);
 }
 
-extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
-				      uint32_t n, int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
-				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
-				      void *d_ws, int grid, hipStream_t stream);
+extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
+				      uint32_t n, int start_id, int mode, void *d_rec, int compact, uint32_t *d_ext,
+				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters, void *d_ws,
+				      int grid, hipStream_t stream);
 
 extern "C" int nsd_launch_dissect(const uint8_t *d_frames, const uint64_t *d_desc, uint32_t n,
 				  int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
 				  uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
 				  void *d_ws, int grid, hipStream_t stream)
 {
-	return nsd_launch_dissect_sll(d_frames, d_desc, nullptr, n, start_id, mode, d_rec, d_ext, ext_words,
+	return nsd_launch_dissect_rec(d_frames, d_desc, nullptr, n, start_id, mode, d_rec, 0, d_ext, ext_words,
 				      d_ext_used, d_counters, d_ws, grid, stream);
 }
 
-// d_sll: one struct sockaddr_ll (nsd_sll_t, 20 bytes) per packet, or NULL
-// (read as zeros); used by the LINKTYPE_LINUX_SLL head only
 extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
 				      uint32_t n, int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
 				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
 				      void *d_ws, int grid, hipStream_t stream)
 {
+	return nsd_launch_dissect_rec(d_frames, d_desc, d_sll, n, start_id, mode, d_rec, 0, d_ext, ext_words,
+				      d_ext_used, d_counters, d_ws, grid, stream);
+}
+
+// d_sll: one struct sockaddr_ll (nsd_sll_t, 20 bytes) per packet, or NULL
+// (read as zeros); used by the LINKTYPE_LINUX_SLL head only.  d_rec: n
+// nsd_rec (16 B), or n nsd_crec (8 B) when `compact`.
+extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
+				      uint32_t n, int start_id, int mode, void *d_rec, int compact, uint32_t *d_ext,
+				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters, void *d_ws,
+				      int grid, hipStream_t stream)
+{
 	using namespace nsd;
+	typedef void (*kfn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, uint32_t *, uint32_t,
+			    uint32_t *, uint32_t, unsigned long long *, uint64_t *, uint32_t, const uint32_t *);
+	static const kfn kernels[2][3] = {
+		{ dissect_all<PRINT_NORM, false>, dissect_all<PRINT_LESS, false>, dissect_all<PRINT_HEX, false> },
+		{ dissect_all<PRINT_NORM, true>, dissect_all<PRINT_LESS, true>, dissect_all<PRINT_HEX, true> },
+	};
 	static int s_cus = 0;
 	if (n == 0)
 		return 0;
@@ -899,18 +942,18 @@ extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d
 	// persistent grid: exactly the blocks that are resident together (CUs x
 	// the kernel's occupancy), so no block waits for a second round; every
 	// block grid-strides (counters then cost one flush per block)
-	static int s_occ[3] = { 0, 0, 0 };
+	static int s_occ[2][3] = { { 0, 0, 0 }, { 0, 0, 0 } };
 	const int mi = mode == PRINT_NORM ? 0 : mode == PRINT_LESS ? 1 : 2;
-	const void *f = mi == 0 ? (const void *)dissect_all<PRINT_NORM>
-		      : mi == 1 ? (const void *)dissect_all<PRINT_LESS>
-				: (const void *)dissect_all<PRINT_HEX>;
-	if (!s_occ[mi]) {
+	const int ci = compact ? 1 : 0;
+	const kfn f = kernels[ci][mi];
+	if (!s_occ[ci][mi]) {
 		int occ = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, BLOCK, 0) != hipSuccess || occ < 1)
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)f, BLOCK, 0) != hipSuccess ||
+		    occ < 1)
 			occ = 4;
-		s_occ[mi] = occ;
+		s_occ[ci][mi] = occ;
 	}
-	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)(s_cus * s_occ[mi]);
+	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)(s_cus * s_occ[ci][mi]);
 	if (cap_blocks > NSD_MAX_GRID)
 		cap_blocks = NSD_MAX_GRID;
 	if (blocks > cap_blocks)
@@ -926,9 +969,8 @@ extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d
 	const uint64_t per = (uint64_t)ext_words / (2ull * blocks * WAVES);
 	const uint32_t lo = NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS), hi = 512 * NSD_EXT_WORDS(16);
 	const uint32_t chunk = (uint32_t)(per < lo ? lo : per > hi ? hi : per) & ~3u;
-	hipLaunchKernelGGL(mi == 0 ? dissect_all<PRINT_NORM> : mi == 1 ? dissect_all<PRINT_LESS> : dissect_all<PRINT_HEX>,
-			   dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id,
-			   (uint4 *)d_rec, d_ext, ext_words, d_ext_used, chunk, (unsigned long long *)d_counters,
-			   pend, region, (const uint32_t *)d_sll);
+	hipLaunchKernelGGL(f, dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec, d_ext,
+			   ext_words, d_ext_used, chunk, (unsigned long long *)d_counters, pend, region,
+			   (const uint32_t *)d_sll);
 	return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -24,6 +24,9 @@ FRAME_PAD = 64
 REC_DTYPE = np.dtype([("chain", "<u4"), ("data_off", "<u2"), ("tail_off", "<u2"),
                       ("ip_csum", "<u2"), ("nflags", "u1"), ("off2", "u1", (5,))])
 REC_BYTES = 16
+# nsd_crec: the compact 8-byte record (chain ids or ext slot, ip_csum, nflags)
+CREC_DTYPE = np.dtype([("chain", "<u4"), ("ip_csum", "<u2"), ("nflags", "u1"), ("rsvd", "u1")])
+CREC_BYTES = 8
 
 # ext pool (include/netsniff_dissect.h "ext pool"): u32 words; an entry is a
 # 4-word header {packet, nlayers, 0, 0} + one word per layer (id | off << 16)
@@ -71,7 +74,8 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_replay_pcap", "nsd_t3_block_desc", "nsd_dissect_device_sll",
                "dissector_entry_batch_sll", "nsd_format_packet_sll", "nsd_format_batch_sll",
                "nsd_pipe_submit_sll", "nsd_pcap_read_batch_sll", "nsd_t3_block_desc_sll",
-               "nsd_replay_pcap_out", "nsd_build_info", "nsd_walk_packet_cpu", "nsd_set_etcdir"]
+               "nsd_replay_pcap_out", "nsd_build_info", "nsd_walk_packet_cpu", "nsd_set_etcdir",
+               "nsd_dissect_device_compact", "nsd_format_batch_compact"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -184,6 +188,11 @@ def lib():
         L.nsd_walk_packet_cpu.argtypes = [_vp, _u32, _int, _int, _vp, _vp, _vp, _u32, _vp]
         L.nsd_set_etcdir.restype = None
         L.nsd_set_etcdir.argtypes = [ctypes.c_char_p]
+        L.nsd_dissect_device_compact.restype = _int
+        L.nsd_dissect_device_compact.argtypes = [_vp, _vp, _vp, _u32, _int, _int, _vp, _vp, _u32, _vp, _vp,
+                                                 _vp, _vp]
+        L.nsd_format_batch_compact.restype = ctypes.c_long
+        L.nsd_format_batch_compact.argtypes = [_vp, _vp, _vp, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]
         L.nsd_replay_pcap.restype = ctypes.c_long
         L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp, _int]
         _lib = L
@@ -234,6 +243,47 @@ def dissect_device(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, rec=
                                      counters.data_ptr(), workspace.data_ptr(), stream)
     _check(rc, "nsd_dissect_device")
     return rec, ext, ext_used, counters
+
+
+def dissect_device_compact(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, crec=None, ext=None,
+                           ext_used=None, counters=None, stream=None, workspace=None, sll=None):
+    """dissect_device writing compact 8-byte records (nsd_crec).  Returns
+    (crec u8[n*8], ext, ext_used, counters) as cuda tensors."""
+    import torch
+    n = desc.numel()
+    dev = desc.device
+    if crec is None:
+        crec = torch.empty(n * CREC_BYTES, dtype=torch.uint8, device=dev)
+    if ext is None:
+        ext = torch.empty(ext_pool_words(n), dtype=torch.int32, device=dev)
+    if ext_used is None:
+        ext_used = torch.zeros(1, dtype=torch.int32, device=dev)
+    if counters is None:
+        counters = torch.zeros(NCOUNTERS, dtype=torch.int64, device=dev)
+    assert ext.element_size() == 4, "the ext pool is u32 words"
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    L = lib()
+    if workspace is None:
+        workspace = torch.empty(L.nsd_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    rc = L.nsd_dissect_device_compact(frames.data_ptr(), desc.data_ptr(),
+                                      None if sll is None else sll.data_ptr(), n, linktype, mode,
+                                      crec.data_ptr(), ext.data_ptr(), ext.numel(), ext_used.data_ptr(),
+                                      counters.data_ptr(), workspace.data_ptr(), stream)
+    _check(rc, "nsd_dissect_device_compact")
+    return crec, ext, ext_used, counters
+
+
+def compact_of(rec):
+    """The compact records (CREC_DTYPE) that carry what 16-byte records do
+    minus the cursors: chain (or the ext slot), ip_csum, nflags."""
+    out = np.zeros(len(rec), dtype=CREC_DTYPE)
+    ext = (rec["nflags"] & 7) == 7
+    slots = rec["off2"][:, :4].copy().view("<u4").reshape(-1)
+    out["chain"] = np.where(ext, slots, rec["chain"])
+    out["ip_csum"] = rec["ip_csum"]
+    out["nflags"] = rec["nflags"]
+    return out
 
 
 def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_words=None, sll=None):
@@ -356,6 +406,32 @@ def format_batch(frames, desc, rec, ext=None, mode=PRINT_NORM, linktype=LINKTYPE
                                        None if sll is None else sll.ctypes.data, n, linktype, mode,
                                        rec.ctypes.data, ext_ptr, ctypes.addressof(out), cap,
                                        ends.ctypes.data, rc.ctypes.data)
+    if total < 0:
+        raise NsdError("format buffer too small")
+    raw = out.raw[:total]
+    texts, prev = [], 0
+    for e in ends:
+        texts.append(raw[prev:int(e)])
+        prev = int(e)
+    return texts, rc
+
+
+def format_batch_compact(frames, desc, crec, ext=None, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, sll=None):
+    """format_batch over compact records (CREC_DTYPE)."""
+    n = len(desc)
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    desc = np.ascontiguousarray(desc, dtype=np.uint64)
+    crec = np.ascontiguousarray(crec, dtype=CREC_DTYPE)
+    ext_keep = None if ext is None or len(ext) == 0 else np.ascontiguousarray(ext).view(np.uint32)
+    ends = np.zeros(n, dtype=np.uint64)
+    rc = np.zeros(n, dtype=np.int8)
+    cap = int(frames.nbytes) * 7 + 1024 * n + 4096
+    out = ctypes.create_string_buffer(cap)
+    sll = None if sll is None else np.ascontiguousarray(sll, dtype=SLL_DTYPE)
+    total = lib().nsd_format_batch_compact(frames.ctypes.data, desc.ctypes.data,
+                                           None if sll is None else sll.ctypes.data, n, linktype, mode,
+                                           crec.ctypes.data, None if ext_keep is None else ext_keep.ctypes.data,
+                                           ctypes.addressof(out), cap, ends.ctypes.data, rc.ctypes.data)
     if total < 0:
         raise NsdError("format buffer too small")
     raw = out.raw[:total]

@@ -83,6 +83,58 @@ def test_synthetic_configs(cfg, n, mode):
     _check(frames, desc, mode)
 
 
+def _check_compact(frames, desc, mode):
+    """Compact device records == the oracle's records minus the cursors; ext
+    chains compared by their entries; counters equal."""
+    import torch
+    f = torch.from_numpy(frames).cuda()
+    d = torch.from_numpy(desc.view(np.int64)).cuda()
+    crec, ext, used, cnt = nsd.dissect_device_compact(f, d, mode=mode)
+    torch.cuda.synchronize()
+    got = crec.cpu().numpy().view(nsd.CREC_DTYPE)
+    dext = ext.cpu().numpy().view(np.uint32)[:int(used.item())]
+    orec, oext, ocnt, _ = T.oracle_records(frames, desc, mode=mode)
+    want = nsd.compact_of(orec)
+    for fld in ("ip_csum", "nflags"):
+        bad = np.nonzero(got[fld] != want[fld])[0]
+        assert len(bad) == 0, f"{fld} differs at {bad[:10]}"
+    inline = (want["nflags"] & 7) != 7
+    assert np.array_equal(got["chain"][inline], want["chain"][inline]), "chain ids differ"
+    for i in np.nonzero(~inline)[0]:
+        if want[i]["chain"] == 0xFFFFFFFF:      # no entry (pool full)
+            assert got[i]["chain"] == 0xFFFFFFFF
+            continue
+        gp, gids, goffs = nsd.ext_entry(dext, int(got[i]["chain"]))
+        _, oids, ooffs = nsd.ext_entry(oext, int(want[i]["chain"]))
+        assert gp == i and (gids, goffs) == (oids, ooffs), f"ext chain differs at {i}"
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt)
+    return got, dext
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_compact_edge_and_leaves(mode):
+    _, leaves = T.read_pcap(T.GOLDEN + "/leaves.pcap")
+    frames, desc = T.batch_from_packets(edge_cases.cases() + leaves, align=2)
+    _check_compact(frames, desc, mode)
+
+
+@pytest.mark.parametrize("cfg", [T.SYN_UDP64, T.SYN_IMIX, T.SYN_IPV6X])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_compact_synthetic_text(cfg, mode):
+    """Device compact records of 64K-packet prefixes -> the host formatter
+    -> the reference text digest (tests/golden/prefix.json)."""
+    import hashlib
+    import json
+    key = {T.SYN_UDP64: "udp64", T.SYN_IMIX: "imix", T.SYN_IPV6X: "ipv6x"}[cfg]
+    frames, desc = T.make_batch(cfg, 65536)
+    crec, ext = _check_compact(frames, desc, mode)
+    texts, rc = nsd.format_batch_compact(frames, desc, crec, ext, mode=mode)
+    assert (rc == 0).all()
+    with open(T.GOLDEN + "/prefix.json") as fh:
+        want = json.load(fh)[f"{key}:m{mode}"]["text_sha256"]
+    assert hashlib.sha256(b"".join(texts)).hexdigest() == want
+
+
 def test_imix_odd_alignment():
     frames, desc = T.make_batch(T.SYN_IMIX, 20000, align=1)
     _check(frames, desc, T.PRINT_NORM)

@@ -115,6 +115,39 @@ def test_formatter_leaves_match_golden(mode):
     assert host >= (2500 if mode == T.PRINT_NORM else 2000) and moved >= 1200, (host, moved)
 
 
+@pytest.mark.parametrize("name", ["tiny", "edge", "leaves"])
+@pytest.mark.parametrize("mode", MODES)
+def test_formatter_compact_matches_golden(name, mode):
+    """Compact 8-byte records (no cursors: each layer starts where the
+    previous print left the cursor) render the reference's text too."""
+    if name == "leaves" and mode not in (T.PRINT_NORM, T.PRINT_LESS):
+        pytest.skip("leaf goldens exist for NORM / LESS")
+    lt, pkts, frames, desc = batch(name)
+    gold = load_golden(f"{name}.m{mode}.w65535")
+    rec, ext, _, _ = T.oracle_records(frames, desc, linktype=lt, mode=mode)
+    crec = nsd.compact_of(rec)
+    texts, rc = nsd.format_batch_compact(frames, desc, crec, ext, mode=mode, linktype=lt)
+    for i in range(len(pkts)):
+        if rec[i]["nflags"] & 0x20:          # overflow: no chain in the record
+            assert rc[i] != 0
+            continue
+        assert rc[i] == 0, f"packet {i}: status {rc[i]}"
+        assert texts[i] == gold[i], f"packet {i} differs"
+
+
+@pytest.mark.parametrize("key,cfg", [("udp64", T.SYN_UDP64), ("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)])
+def test_prefix_text_formatter_compact(key, cfg):
+    """Compact records of 64K prefixes render the nsref text digests."""
+    with open(os.path.join(G, "prefix.json")) as f:
+        want = json.load(f)
+    frames, desc = T.make_batch(cfg, 65536)
+    for m in (T.PRINT_NORM, T.PRINT_LESS):
+        rec, ext, _, _ = T.oracle_records(frames, desc, mode=m)
+        texts, rc = nsd.format_batch_compact(frames, desc, nsd.compact_of(rec), ext, mode=m)
+        assert (rc == 0).all()
+        assert hashlib.sha256(b"".join(texts)).hexdigest() == want[f"{key}:m{m}"]["text_sha256"]
+
+
 @pytest.mark.parametrize("name", ["tiny", "edge"])
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
 def test_wrap_matches_golden(name, mode):

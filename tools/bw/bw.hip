@@ -76,6 +76,40 @@ __global__ void k_shape_nt(const uint4 *__restrict__ frames, const uint64_t *__r
 	}
 }
 
+// the dissect kernel's staging order: per wave instruction, 4 consecutive
+// lanes read one packet's 4 chunks (1 KiB contiguous per instruction), one
+// record per packet stored by the lane that owns it; REC = 16 or 8 bytes
+template <int REC>
+__global__ void k_shape_coal(const uint4 *__restrict__ frames, const uint64_t *__restrict__ desc,
+			     uint4 *__restrict__ rec, size_t npkt)
+{
+	const int lane = threadIdx.x & 63;
+	for (size_t base = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) & ~(size_t)63; base < npkt;
+	     base += (size_t)gridDim.x * blockDim.x) {
+		uint32_t acc = 0;
+#pragma unroll
+		for (int r = 0; r < 4; r++) {
+			const size_t t = base * 4 + r * 64 + lane;   // chunk index
+			if (t < npkt * 4) {
+				const uint4 v = ntl(frames + t);
+				acc ^= v.x ^ v.y ^ v.z ^ v.w;
+			}
+		}
+		acc ^= __shfl_xor(acc, 1, 64) ^ __shfl_xor(acc, 2, 64);
+		const size_t i = base + lane;
+		if (i < npkt) {
+			const uint64_t d = desc[i];
+			if (REC == 16) {
+				nts(make_uint4(acc ^ (uint32_t)d, acc, 0, 0), rec + i);
+			} else {
+				typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+				const v2u v = { acc ^ (uint32_t)d, acc };
+				__builtin_nontemporal_store(v, (v2u *)rec + i);
+			}
+		}
+	}
+}
+
 int main()
 {
 	const size_t bytes = 1ull << 30;
@@ -131,8 +165,22 @@ int main()
 			CHECK(hipEventElapsedTime(&ms, e0, e1));
 			nt[v] = (double)(n / 4) * 88 / (ms / 5 * 1e-3) / 1e9;
 		}
-		printf("{\"blocks_per_cu\": %d, \"read_gbs\": %.1f, \"write_gbs\": %.1f, \"copy_gbs\": %.1f, \"pass1_shape_gbs\": %.1f, \"shape_ntload\": %.1f, \"shape_ntstore\": %.1f, \"shape_nt_both\": %.1f}\n",
-		       grids[gi], gbs[0], gbs[1], gbs[2], gbs[3], nt[0], nt[1], nt[2]);
+		double co[2];
+		for (int v = 0; v < 2; v++) {
+			for (int rep = 0; rep < 6; rep++) {
+				if (rep == 1)
+					CHECK(hipEventRecord(e0));
+				if (v == 0) hipLaunchKernelGGL((k_shape_coal<16>), dim3(grid), dim3(256), 0, 0, a, d, b, n / 4);
+				if (v == 1) hipLaunchKernelGGL((k_shape_coal<8>), dim3(grid), dim3(256), 0, 0, a, d, b, n / 4);
+			}
+			CHECK(hipEventRecord(e1));
+			CHECK(hipEventSynchronize(e1));
+			CHECK(hipEventElapsedTime(&ms, e0, e1));
+			co[v] = (double)(n / 4) * (v == 0 ? 88 : 80) / (ms / 5 * 1e-3) / 1e9;
+		}
+		printf("{\"blocks_per_cu\": %d, \"read_gbs\": %.1f, \"write_gbs\": %.1f, \"copy_gbs\": %.1f, \"pass1_shape_gbs\": %.1f, \"shape_ntload\": %.1f, \"shape_ntstore\": %.1f, \"shape_nt_both\": %.1f, \"coal_rec16_gbs\": %.1f, \"coal_rec8_gbs\": %.1f, \"coal_rec16_ms_per_16M\": %.4f, \"coal_rec8_ms_per_16M\": %.4f}\n",
+		       grids[gi], gbs[0], gbs[1], gbs[2], gbs[3], nt[0], nt[1], nt[2], co[0], co[1],
+		       16777216.0 * 88 / co[0] / 1e6, 16777216.0 * 80 / co[1] / 1e6);
 	}
 	return 0;
 }

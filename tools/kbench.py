@@ -27,19 +27,22 @@ def main():
     ap.add_argument("--packets", type=int, default=1 << 24)
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--records", default="both", choices=["compact", "full", "both"])
     args = ap.parse_args()
     import bench
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
+    forms = {"compact": [True], "full": [False], "both": [False, True]}[args.records]
     for key in args.configs.split(","):
-        b = bench.Batch(key, args.packets, 0, 1, dev)
-        ms = bench.time_steps(b, args.mode, args.steps, args.warmup, args.grid)
-        cnt = b.counters.cpu().numpy().view(np.uint64)
-        r = b.roofline(ms)
-        print(f"{key:6s} kernel_ms={ms:.4f} frac={r['frac'] if r else None} read_frac={r['read_frac'] if r else None}"
-              f" pkts_counted={int(cnt[32])}", flush=True)
-        b.free()
-        torch.cuda.empty_cache()
+        for compact in forms:
+            b = bench.Batch(key, args.packets, 0, 1, dev, compact=compact)
+            ms = bench.time_steps(b, args.mode, args.steps, args.warmup, 0 if compact else args.grid)
+            cnt = b.counters.cpu().numpy().view(np.uint64)
+            r = b.roofline(ms)
+            print(f"{key:6s} rec{b.rec_b:<2d} kernel_ms={ms:.4f} frac={r['frac'] if r else None} "
+                  f"read_frac={r['read_frac'] if r else None} pkts_counted={int(cnt[32])}", flush=True)
+            b.free()
+            torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
