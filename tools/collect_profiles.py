@@ -1,16 +1,19 @@
 """Turn a tools/gpu_round.sh run (gpurun_out/round/) into the committed
 profile files:
 
-  profiles/<tag>_bench_<cfg>.json         the bench JSON line
-  profiles/<tag>_<cfg>_kernel_stats.csv   rocprofv3 --stats summary
-  profiles/pmc_<cfg>.json                 HBM bytes per dissect call (read by bench.py)
+  profiles/<tag>_bench_default.json    the default bench JSON line (C2 headline,
+                                       C3/C4 legs, both record forms, in-run PMC
+                                       traffic, CPU baseline, e2e, replay, BPF)
+  profiles/<tag>_bench_c5_one_gpu.json C5's 128M IMIX packets on one GPU
+  profiles/<tag>_kernel_stats.csv      rocprofv3 --kernel-trace --stats of the
+                                       default bench command (--no-pmc)
+  profiles/<tag>_kernel_check.json     per dissect_all instantiation: rocprof
+                                       average vs the bench's HIP-event time
+  profiles/<tag>_pytest_gpu.log, <tag>_smoke.log
 
-HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE come
-from separate --pmc passes, in KiB; FETCH_SIZE counts half the bytes of a
-wide (16 B/lane) coalesced read on gfx950, so it is doubled; WRITE_SIZE is
-exact for 16 B/lane stores.  A dissect call is one dissect_all launch (pass 1,
-pass 2 and the ICMPv4 checksums as phases of one kernel); the BPF filter
-kernels are reported separately (bpf_filter)."""
+The bench's `traffic` comes from its own two rocprofv3 --pmc child passes
+(FETCH_SIZE doubled: the gfx950 wide-read correction; WRITE_SIZE exact;
+MI355X_MICROARCH.md "HBM")."""
 import csv
 import json
 import os
@@ -18,56 +21,75 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PACKETS = 1 << 24
 
 
-def counter_sum(path, counter, kernel="nsd::dissect_all"):
-    total, calls = 0.0, 0
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            name = row["Kernel_Name"]
-            if kernel not in name or row["Counter_Name"] != counter:
-                continue
-            total += float(row["Counter_Value"])
-            calls += 1
-    return total, calls
+def last_json(path):
+    if not os.path.exists(path):
+        return None
+    for line in reversed(open(path).read().strip().splitlines()):
+        if line.startswith("{"):
+            return line
+    return None
 
 
 def main(tag, src=os.path.join(ROOT, "gpurun_out", "round")):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    for cfg in ("udp64", "imix", "ipv6x"):
-        log = os.path.join(src, f"bench_{cfg}.log")
-        if os.path.exists(log):
-            line = open(log).read().strip().splitlines()[-1]
+    for name, out in (("bench_default.log", "bench_default.json"), ("bench_c5.log", "bench_c5_one_gpu.json")):
+        line = last_json(os.path.join(src, name))
+        if line:
             json.loads(line)
-            with open(os.path.join(prof, f"{tag}_bench_{cfg}.json"), "w") as f:
+            with open(os.path.join(prof, f"{tag}_{out}"), "w") as f:
                 f.write(line + "\n")
-        st = os.path.join(src, f"stats_{cfg}", "run_kernel_stats.csv")
-        if os.path.exists(st):
-            shutil.copy(st, os.path.join(prof, f"{tag}_{cfg}_kernel_stats.csv"))
-        fp = os.path.join(src, f"pmc_{cfg}_FETCH_SIZE", "run_counter_collection.csv")
-        wp = os.path.join(src, f"pmc_{cfg}_WRITE_SIZE", "run_counter_collection.csv")
-        if os.path.exists(fp) and os.path.exists(wp):
-            fk, fc = counter_sum(fp, "FETCH_SIZE")
-            wk, wc = counter_sum(wp, "WRITE_SIZE")
-            read_b = 2 * fk * 1024 / fc
-            write_b = wk * 1024 / wc
-            res = {"tag": tag, "calls": [fc, wc], "FETCH_SIZE_KiB_per_call": fk / fc,
-                   "WRITE_SIZE_KiB_per_call": wk / wc, "read_bytes_corrected": read_b,
-                   "write_bytes": write_b, "hbm_bytes_per_launch": read_b + write_b,
-                   "bytes_per_packet": (read_b + write_b) / PACKETS,
-                   "note": "per dissect_all launch; read = 2 x FETCH_SIZE "
-                           "(gfx950 wide-read correction), KiB -> bytes"}
-            bk, bc = counter_sum(fp, "FETCH_SIZE", "bpf_filter<false>")
-            bw, bwc = counter_sum(wp, "WRITE_SIZE", "bpf_filter<false>")
-            if bc and bwc:
-                res["bpf_filter"] = {"read_bytes_corrected": 2 * bk * 1024 / bc, "write_bytes": bw * 1024 / bwc,
-                                     "hbm_bytes_per_launch": 2 * bk * 1024 / bc + bw * 1024 / bwc,
-                                     "launches": [bc, bwc]}
-            with open(os.path.join(prof, f"pmc_{cfg}.json"), "w") as f:
-                json.dump(res, f, indent=1)
-            print(cfg, json.dumps(res))
+    for name in ("pytest_gpu.log", "smoke.log"):
+        p = os.path.join(src, name)
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(prof, f"{tag}_{name}"))
+    st = os.path.join(src, "stats", "run_kernel_stats.csv")
+    if os.path.exists(st):
+        shutil.copy(st, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+        rows = {}
+        with open(st) as f:
+            for row in csv.DictReader(f):
+                if "dissect_all" in row["Name"]:
+                    rows[row["Name"]] = {"calls": int(row["Calls"]),
+                                         "average_us": float(row["AverageNs"]) / 1e3}
+        bench = last_json(os.path.join(src, "stats.log"))
+        check = {"rocprof_stats": rows}
+        # per workload: the bench launches dissect_all in this order, warmup +
+        # steps each: headline (compact), other record form, then each leg
+        tr = os.path.join(src, "stats", "run_kernel_trace.csv")
+        if os.path.exists(tr) and bench:
+            b = json.loads(bench)
+            per = b["steps"] + b["warmup"]
+            d = {}
+            with open(tr) as f:
+                for row in csv.DictReader(f):
+                    if "dissect_all" in row["Kernel_Name"]:
+                        d.setdefault(row["Kernel_Name"].split("(")[0], []).append(
+                            (int(row["Dispatch_Id"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3))
+            names = ["headline"] + list((b.get("legs") or {}).keys())
+            compact = sorted(d.get("void nsd::dissect_all<0, true>", []))
+            full = sorted(d.get("void nsd::dissect_all<0, false>", []))
+            split = {}
+            for k, name in enumerate(names):
+                seg = compact[k * per:(k + 1) * per][b["warmup"]:]
+                if seg:
+                    split[name] = round(sum(x for _, x in seg) / len(seg), 1)
+            if full:
+                seg = full[b["warmup"]:]
+                split["other_records"] = round(sum(x for _, x in seg) / len(seg), 1)
+            check["rocprof_trace_avg_us"] = split
+        if bench:
+            b = json.loads(bench)
+            check["bench_kernel_ms"] = {"headline": b["roofline"]["kernel_ms"] if b.get("roofline") else None}
+            for k, leg in (b.get("legs") or {}).items():
+                check["bench_kernel_ms"][k] = leg["roofline"]["kernel_ms"] if leg.get("roofline") else None
+            if b.get("other_records") and b["other_records"].get("roofline"):
+                check["bench_kernel_ms"]["other_records"] = b["other_records"]["roofline"]["kernel_ms"]
+        with open(os.path.join(prof, f"{tag}_kernel_check.json"), "w") as f:
+            json.dump(check, f, indent=1)
+        print(json.dumps(check, indent=1))
 
 
 if __name__ == "__main__":
