@@ -135,6 +135,34 @@ def test_compact_synthetic_text(cfg, mode):
     assert hashlib.sha256(b"".join(texts)).hexdigest() == want
 
 
+def _long_chains(n, seed=11):
+    """IPv6 with 2..7 Hop-by-Hop / DestOpts headers of 8..128 bytes each: most
+    chains run past several 128-byte continuation windows and past the
+    record's 6 layers (ext entries from the per-wave chunks)."""
+    import random
+    rnd = random.Random(seed)
+    E = edge_cases
+    pkts = []
+    for _ in range(n):
+        k = rnd.randint(2, 7)
+        kinds = [rnd.choice([0, 60]) for _ in range(k)]
+        body = b""
+        for j in range(k):
+            nh = kinds[j + 1] if j + 1 < k else 17
+            hl = rnd.randint(0, 15)
+            body += bytes([nh, hl]) + bytes(rnd.randrange(256) for _ in range((hl + 1) * 8 - 2))
+        body += E.udp(payload=bytes(rnd.randrange(8)))
+        pkts.append(E.eth(0x86DD) + E.ipv6(kinds[0], len(body)) + body)
+    return pkts
+
+
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_long_ext_chains(mode):
+    frames, desc = T.batch_from_packets(_long_chains(30000), align=2)
+    rec, _ = _check(frames, desc, mode)
+    assert ((rec["nflags"] & 7) == 7).mean() > 0.3      # many chains past 6 layers
+
+
 def test_imix_odd_alignment():
     frames, desc = T.make_batch(T.SYN_IMIX, 20000, align=1)
     _check(frames, desc, T.PRINT_NORM)
