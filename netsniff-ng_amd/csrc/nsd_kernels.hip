@@ -700,13 +700,23 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			pq.npend += (uint32_t)__popcll(pmask);
 		}
 		// per-ops counts from the finished chains, grouped by chain word
-		// (ids are >= 1, so equal chain words imply equal layer counts)
+		// (ids are >= 1, so equal chain words imply equal layer counts) for
+		// the first two distinct chains of the tile (C2: one), the rest per
+		// lane (C3: -4.5 % against looping over every distinct chain)
 		{
 			uint32_t key = done ? w.chain : 0xFFFFFFFFu;
-			for (;;) {
+			for (int it = 0;; it++) {
 				const uint64_t pm = __ballot(key != 0xFFFFFFFFu);
 				if (!pm)
 					break;
+				if (it == 2) {
+					// more than two distinct chains in the tile: the rest
+					// count their own layers (the LDS serialises them)
+					if (key != 0xFFFFFFFFu)
+						for (uint32_t k = 0; k < w.n; k++)
+							atomicAdd(&s_cnt[NSD_CNT_OPS + ((key >> (5 * k)) & 31)], 1ull);
+					break;
+				}
 				const int leader = __ffsll((unsigned long long)pm) - 1;
 				const uint32_t lk = __shfl(key, leader, 64);
 				const uint64_t m = __ballot(key == lk);
