@@ -177,7 +177,8 @@ struct LSrc {
 		if (!(r & 1) && in_window(o, 2 * nwords) && (FAST || o + 2 * nwords <= caplen)) {
 			uint32_t j = r >> 2, k = nwords;
 			if ((r & 2) && k) { sum += dw(j) >> 16; j++; k--; }
-			for (; k >= 2; k -= 2, j++) { const uint32_t v = dw(j); sum += (v & 0xFFFF) + (v >> 16); }
+			for (; k >= 2; k -= 2, j++)
+				sum = __builtin_amdgcn_sad_u16(dw(j), 0u, sum);   // + both 16-bit halves
 			if (k) sum += dw(j) & 0xFFFF;
 			return sum;
 		}
@@ -195,49 +196,43 @@ struct LSrc {
 template <int WIN>
 struct Chunks {
 	static constexpr int CPP = WIN / 16;   // 16-byte chunks per window
-	static_assert(CPP * 6 <= 64, "chunk valid counts must fit one word");
+	static_assert(CPP <= 4 && WIN <= 255, "a chunk's valid count per byte of nv");
 	uint4 v[CPP];
-	uint64_t nv;   // valid bytes of chunk r (0..16) in bits 6r..6r+5
+	uint32_t nv;   // valid bytes of chunk r (0..16) in byte r
 };
 
 // issue the loads (no wait): in round r, lane (q * CPP + c) % 64 loads chunk
-// c of packet q's window = aligned bytes [A_q + wb_q + 16c, +16), skipped when
-// the chunk lies wholly past caplen (or the packet does not participate).
-// Only the descriptor (and, with WB, the window base) is shuffled; the count
-// of valid bytes per chunk is kept for stage_write, which then needs no
-// shuffles.  my_wbp: window base (multiple of 16) | 0x80000000 when not
-// participating; without WB every packet with caplen > 0 participates at 0.
-template <bool WB, int WIN>
-__device__ __forceinline__ void stage_load(Chunks<WIN> &ch, const uint8_t *frames, uint64_t my_desc,
-					   uint32_t my_wbp, int lane)
+// c of packet q's window = aligned bytes [A_q + 16c, +16), skipped when the
+// chunk lies wholly past caplen.  Each lane prepares its own packet's
+// aligned start address and frame end once; two shuffles per round hand
+// them to the loading lanes (the end, capped at 255 - the window is shorter
+// - rides in the address's high dword, a 48-bit VA leaves its top byte
+// free).  The count of valid bytes per chunk is kept for stage_write.
+template <int WIN>
+__device__ __forceinline__ void stage_load(Chunks<WIN> &ch, const uint8_t *frames, uint64_t my_desc, int lane)
 {
 	constexpr int CPP = Chunks<WIN>::CPP;
+	const uint64_t a = (uint64_t)frames + (NSD_DESC_OFF(my_desc) & ~15ull);
+	const uint32_t lim = (uint32_t)NSD_DESC_CAPLEN(my_desc) + ((uint32_t)my_desc & 15);
+	const uint32_t hr = (uint32_t)(a >> 32) | (lim < 255u ? lim : 255u) << 24;
 	ch.nv = 0;
 #pragma unroll
 	for (int r = 0; r < CPP; r++) {
 		const int t = r * 64 + lane;
 		const int q = t / CPP, c = t % CPP;
-		const uint32_t dlo = __shfl((uint32_t)my_desc, q, 64);
-		const uint32_t dhi = __shfl((uint32_t)(my_desc >> 32), q, 64);
-		uint32_t pos = 16u * c;
-		bool part = true;
-		if constexpr (WB) {
-			const uint32_t wbp = __shfl(my_wbp, q, 64);
-			part = !(wbp >> 31);
-			pos += wbp & 0x7FFFFFFFu;
-		}
-		const uint32_t lim = (dhi >> 8) + (dlo & 15);   // first aligned position past the frame
-		const uint32_t nv = part && pos < lim ? min(lim - pos, 16u) : 0u;
-		const uint64_t off = ((uint64_t)(dhi & 0xFF) << 32) | dlo;
+		const uint32_t alo = __shfl((uint32_t)a, q, 64), ahr = __shfl(hr, q, 64);
+		const uint32_t pos = 16u * c, qlim = ahr >> 24;
+		const uint32_t nv = qlim > pos ? min(qlim - pos, 16u) : 0u;
 		if (nv) {
 			// streaming loads (nt): C2 -9 %, C3 -2 %; C4 +5 % (its general
 			// walk re-reads the first line from HBM rather than L2)
-			const v4u t = __builtin_nontemporal_load((const v4u *)(frames + (off & ~15ull) + pos));
-			ch.v[r] = make_uint4(t.x, t.y, t.z, t.w);
+			const uint64_t src = ((uint64_t)(ahr & 0xFFFFFFu) << 32 | alo) + pos;
+			const v4u t4 = __builtin_nontemporal_load((const v4u *)src);
+			ch.v[r] = make_uint4(t4.x, t4.y, t4.z, t4.w);
 		} else {
 			ch.v[r] = make_uint4(0, 0, 0, 0);
 		}
-		ch.nv |= (uint64_t)nv << (6 * r);
+		ch.nv |= nv << (8 * r);
 	}
 }
 
@@ -251,7 +246,7 @@ __device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks<WIN> &c
 	for (int r = 0; r < CPP; r++) {
 		const int t = r * 64 + lane;
 		const int q = t / CPP, c = t % CPP;
-		const uint32_t nv = (uint32_t)(ch.nv >> (6 * r)) & 0x3F;
+		const uint32_t nv = (ch.nv >> (8 * r)) & 0xFF;
 		uint32_t w[4] = { ch.v[r].x, ch.v[r].y, ch.v[r].z, ch.v[r].w };
 		if (nv < 16) {
 #pragma unroll
@@ -662,7 +657,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
 	uint64_t d1 = (base + stride < n && base + stride + lane < n) ? desc[base + stride + lane] : 0;
 	Chunks<WIN1> ch;
-	stage_load<false, WIN1>(ch, frames, d0, 0, lane);
+	stage_load<WIN1>(ch, frames, d0, lane);
 
 	for (; base < n; base += stride) {
 		const uint32_t i = base + lane;
@@ -676,7 +671,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
 		const uint32_t b1 = base + stride;
 		if (b1 < n)
-			stage_load<false, WIN1>(ch, frames, d1, 0, lane);
+			stage_load<WIN1>(ch, frames, d1, lane);
 		wave_sync_lds();
 
 		WalkOut w;
