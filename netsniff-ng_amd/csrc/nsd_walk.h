@@ -379,62 +379,93 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 		g.layer(w, k, id, start);
 	w.n = act ? k + 1 : k;
 
-	// ---- parse (bytes >= caplen read as zero).  Everything below is
-	// computed for every lane and selected by the rule kind; boolean terms
-	// are combined with & and | so the compiler keeps them as selects.
+	// ---- parse (bytes >= caplen read as zero).  The common rules are
+	// computed for every lane and selected by the rule kind (boolean terms
+	// combined with & and | so the compiler keeps them as selects).
 	const uint32_t len = w.tail - start;   // pkt_len (pkt_buff.h:36-41)
 	const uint32_t info = s.step(id);
 	const uint32_t minl = info & 0xFF, fadv = (info >> 8) & 0xFF, kind = (info >> 16) & 0xF,
 		       kpos = (info >> 20) & 0xF;
 	const bool kw16 = (info >> 24) & 1;
 	const uint32_t B0 = s.dword_at(start);          // layer bytes 0..3
-	const uint32_t KD = s.dword_at(start + kpos);   // the next-ops key's bytes
+	// the next-ops key's bytes: the layer's first byte for the extension
+	// headers (kpos 0), a second read only when a lane's key sits further on
+	uint32_t KD = B0;
+	if (g.any(act & (kpos != 0)))
+		KD = s.dword_at(start + kpos);
 	const uint32_t b0 = B0 & 0xFF, b1 = (B0 >> 8) & 0xFF, b2 = (B0 >> 16) & 0xFF;
-	const uint32_t k2 = __builtin_bswap16((uint16_t)(B0 >> 16));   // IPv4 tot_len
-	const uint32_t key16 = __builtin_bswap16((uint16_t)KD);
-	const uint32_t e2 = s.l2h(NSD_L2H(key16));
-	// eth_lay2 / eth_lay3 (dissector_eth.c:30-62)
-	const int nx = kw16 ? ((e2 & 0xFFFF) == key16 ? (int)(e2 >> 16) : 0) : s.lay3(KD & 0xFF);
+	// eth_lay2 (a 16-bit ethertype; the perfect hash) / eth_lay3 (dissector_eth.c:30-62)
+	int nx = s.lay3(KD & 0xFF);
+	if (g.any(act & kw16)) {
+		const uint32_t key16 = __builtin_bswap16((uint16_t)KD);
+		const uint32_t e2 = s.l2h(NSD_L2H(key16));
+		nx = kw16 ? ((e2 & 0xFFFF) == key16 ? (int)(e2 >> 16) : 0) : nx;
+	}
 	const uint32_t T8 = (b1 + 1u) * 8u;             // (hdr_ext_len + 1) * 8
+	const bool pulled = len >= minl;
 
 	// HBH / DestOpts: opt_len = T8 - 2 <= pkt_len after the 2-byte pull;
-	// Routing: data_len = T8 - 4 <= pkt_len after the 4-byte pull
+	// Routing: data_len = T8 - 4 <= pkt_len after the 4-byte pull.  These,
+	// the fixed pulls and the leaves are the common case; the other kinds'
+	// rules run behind wave-uniform branches (only when a lane of the wave
+	// is on such a layer: VALU issue bounds the general walk)
 	const bool t8ok = T8 <= len;
-	// IPv4: options pulled if present, else data stays (proto_ipv4.c:136)
-	const uint32_t ihl = b0 & 0xF;
-	const uint32_t opts = (ihl > 5 ? ihl : 5) * 4u - 20u;
-	const uint32_t v4adv = 20 + (opts <= len - 20 ? opts : 0);
-	// AH: hdr_len = plen*4 + 8, checked after the 12-byte pull, ICV pulled
-	const uint32_t hl = b1 * 4u + 8u;
-	const bool ahok = hl <= len - 12;
-	const uint32_t ahadv = 12 + ((ahok & (hl > 12)) ? hl - 12 : 0);
-	// Mobility: msg_len check, then (PRINT_NORM) get_mh_type's subtype pull
-	// and the second check
-	const int32_t mdl0 = (int32_t)T8 - 6;
-	const uint32_t l0 = len - 6;
-	const bool mok1 = mdl0 <= (int32_t)l0;
-	const uint32_t sub = b2 < 8 ? (uint32_t)(NSD_MH_SUB >> (8 * b2)) & 0xFF : 0u;
-	const bool sok = sub <= l0;
-	const uint32_t sp = sok ? sub : 0u;
-	const int32_t mdl = mdl0 - ((sok | (b2 <= 5)) ? (int32_t)sub : 0);
-	const bool mok2 = (mdl <= (int32_t)(l0 - sp)) & (mdl >= 0);
-	const bool mobok = MODE == PRINT_NORM ? mok1 & mok2 : mok1;
-	const uint32_t mobadv = !mok1 ? 6u : MODE != PRINT_NORM ? T8 : mok2 ? 6 + sp + (uint32_t)mdl : 6 + sp;
-	// ICMPv6 (PRINT_NORM): types 130-154 have variable-length bodies (host
-	// renders); types 1-4 / 128 / 129 pull a 4-byte body
-	const bool i6host = MODE == PRINT_NORM && b0 - 130u <= 24u;
-	const bool i6body = MODE == PRINT_NORM && ((b0 - 1u <= 3u) | ((b0 & 0xFE) == 128)) & (len >= 8);
-	const uint32_t i6adv = i6host ? 0u : i6body ? 8u : 4u;
-	uint32_t adv = fadv;
-	adv = kind == K_T8 ? (t8ok ? T8 : minl) : adv;
-	adv = kind == K_AH ? ahadv : adv;
-	adv = kind == K_IPV4 ? v4adv : adv;
-	adv = kind == K_MOB ? mobadv : adv;
-	adv = kind == K_ICMP6 ? i6adv : adv;
-	const bool cont = (kind == K_CONT) | (kind == K_IPV4) | ((kind == K_T8) & t8ok) |
-			  ((kind == K_AH) & ahok) | ((kind == K_MOB) & mobok);
-	const bool pulled = len >= minl;
-	const bool host = pulled & ((kind == K_HOST) | ((kind == K_ICMP6) & i6host));
+	uint32_t adv = kind == K_T8 ? (t8ok ? T8 : minl) : fadv;
+	bool cont = (kind == K_CONT) | ((kind == K_T8) & t8ok);
+	bool host = kind == K_HOST;
+	const bool isv4 = act & (kind == K_IPV4);
+	uint32_t ihl = 0;
+	if (g.any(isv4)) {
+		// IPv4: options pulled if present, else data stays (proto_ipv4.c:136)
+		ihl = b0 & 0xF;
+		const uint32_t opts = (ihl > 5 ? ihl : 5) * 4u - 20u;
+		const uint32_t v4adv = 20 + (opts <= len - 20 ? opts : 0);
+		adv = isv4 ? v4adv : adv;
+		cont = cont | isv4;
+		if (MODE == PRINT_NORM) {
+			// tail trim to tot_len - ihl*4, evaluated in size_t (:174-175)
+			const uint32_t k2 = __builtin_bswap16((uint16_t)(B0 >> 16));   // tot_len
+			const int64_t x = (int64_t)k2 - (int64_t)ihl * 4;
+			const bool trim = isv4 & pulled & (x >= 0) & ((uint64_t)x < len - v4adv);
+			w.tail = trim ? start + v4adv + (uint32_t)x : w.tail;
+		}
+	}
+	const bool isah = act & (kind == K_AH);
+	if (g.any(isah)) {
+		// AH: hdr_len = plen*4 + 8, checked after the 12-byte pull, ICV pulled
+		const uint32_t hl = b1 * 4u + 8u;
+		const bool ahok = hl <= len - 12;
+		adv = isah ? 12 + ((ahok & (hl > 12)) ? hl - 12 : 0) : adv;
+		cont = cont | (isah & ahok);
+	}
+	const bool ismob = act & (kind == K_MOB);
+	if (g.any(ismob)) {
+		// Mobility: msg_len check, then (PRINT_NORM) get_mh_type's subtype
+		// pull and the second check
+		const int32_t mdl0 = (int32_t)T8 - 6;
+		const uint32_t l0 = len - 6;
+		const bool mok1 = mdl0 <= (int32_t)l0;
+		const uint32_t sub = b2 < 8 ? (uint32_t)(NSD_MH_SUB >> (8 * b2)) & 0xFF : 0u;
+		const bool sok = sub <= l0;
+		const uint32_t sp = sok ? sub : 0u;
+		const int32_t mdl = mdl0 - ((sok | (b2 <= 5)) ? (int32_t)sub : 0);
+		const bool mok2 = (mdl <= (int32_t)(l0 - sp)) & (mdl >= 0);
+		const bool mobok = MODE == PRINT_NORM ? mok1 & mok2 : mok1;
+		const uint32_t mobadv =
+			!mok1 ? 6u : MODE != PRINT_NORM ? T8 : mok2 ? 6 + sp + (uint32_t)mdl : 6 + sp;
+		adv = ismob ? mobadv : adv;
+		cont = cont | (ismob & mobok);
+	}
+	const bool isi6 = act & (kind == K_ICMP6);
+	if (g.any(isi6)) {
+		// ICMPv6 (PRINT_NORM): types 130-154 have variable-length bodies
+		// (leaf walk); types 1-4 / 128 / 129 pull a 4-byte body
+		const bool i6host = MODE == PRINT_NORM && b0 - 130u <= 24u;
+		const bool i6body = MODE == PRINT_NORM && ((b0 - 1u <= 3u) | ((b0 & 0xFE) == 128)) & (len >= 8);
+		adv = isi6 ? (i6host ? 0u : i6body ? 8u : 4u) : adv;
+		host = host | (isi6 & i6host);
+	}
+	host = host & pulled;
 	const bool upd = act & (kind != K_MPLS);
 	w.data = upd ? start + (pulled ? adv : 0u) : w.data;
 	w.id = upd ? ((pulled & cont) ? nx : 0) : w.id;
@@ -443,12 +474,6 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	// (nsd_leaf.h), so the exit op's dump starts from the record; the
 	// sink decides when (the device walks it after the chain, emit_general)
 	g.template leaf<MODE>(s, upd & host, w, id, start);
-	if (MODE == PRINT_NORM) {
-		// tail trim to tot_len - ihl*4, evaluated in size_t (:174-175)
-		const int64_t x = (int64_t)k2 - (int64_t)ihl * 4;
-		const bool trim = upd & (kind == K_IPV4) & pulled & (x >= 0) & ((uint64_t)x < len - adv);
-		w.tail = trim ? start + adv + (uint32_t)x : w.tail;
-	}
 	// ---- the rare heavy bodies, behind wave-uniform branches
 	const bool v4 = upd && kind == K_IPV4 && pulled;
 	if (MODE == PRINT_NORM && g.any(v4)) {
