@@ -113,6 +113,8 @@ class Batch:
         self.line_bytes = int(np.minimum(caps, 64).sum())   # first 64-B line per frame (BPF leg)
         del desc_np
         ext_w = nsd.ext_pool_words(self.n) if key == "ipv6x" else nsd.ext_pool_words(self.n // 64)
+        if compact:
+            ext_w += self.n   # the side words (compact records of 7..12 layers)
         self.rec = torch.empty(self.n * self.rec_b, dtype=torch.uint8, device=dev)
         self.ext = torch.empty(ext_w, dtype=torch.int32, device=dev)
         self.ext_used = torch.zeros(1, dtype=torch.int32, device=dev)

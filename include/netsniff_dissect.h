@@ -393,15 +393,25 @@ int nsd_walk_packet_cpu(const uint8_t *pkt, uint32_t caplen, int linktype, int m
  * layer (every proto_*.c print pulls its own header), so a consumer that
  * renders, as the reference does for every packet, loses nothing; the
  * 16-byte nsd_rec additionally lets it cross-check the device's cursors.
- * Layout: chain = the ops ids as in nsd_rec (5 bits each, layer count in
- * nflags & 7), or, when (nflags & 7) == NSD_N_EXT, the ext pool slot of the
- * chain (0xFFFFFFFF with NSD_F_OVERFLOW: pool full / chain too long); the
- * ext entry keeps its layer offsets.  nflags, ip_csum: as in nsd_rec.  */
+ * Layout (no layer offsets, so a layer past byte 510 needs no ext form):
+ *  - up to 6 layers: chain = the ops ids as in nsd_rec, nflags & 7 = count;
+ *  - 7..NSD_CREC_MAX_LAYERS layers: chain = ids 0..5, nflags & 7 =
+ *    NSD_N_EXT, nlayers = the count, and the batch's ext pool word i (the
+ *    packet's side word) holds ids 6.. (5 bits each).  Words [0, n) of the
+ *    pool are the side words when ext_words >= n (otherwise such records get
+ *    NSD_F_OVERFLOW); pool entries start at word n + *d_ext_used;
+ *  - longer chains: chain = the ext pool slot (0xFFFFFFFF with
+ *    NSD_F_OVERFLOW: pool full), nflags & 7 = NSD_N_EXT, nlayers = 0; the
+ *    entry keeps ids and layer offsets.
+ * nflags (besides the count), ip_csum: as in nsd_rec.  The counters are the
+ * same as for 16-byte records (NSD_CNT_EXT counts the chains that need the
+ * 16-byte record's ext form). */
+#define NSD_CREC_MAX_LAYERS  12
 typedef struct nsd_crec {
 	uint32_t chain;
 	uint16_t ip_csum;
 	uint8_t  nflags;
-	uint8_t  rsvd;
+	uint8_t  nlayers;
 } nsd_crec;
 
 /* nsd_dissect_device_ws / _sll writing n compact records; d_sll as in

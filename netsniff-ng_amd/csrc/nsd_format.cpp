@@ -1098,9 +1098,9 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 	return format_chain(o, f, linktype, mode, n, ids, offs, end, rec.ip_csum, rec.nflags, sll);
 }
 
-// the same over a compact record: the layer starts come from the prints
+// the same over compact record i: the layer starts come from the prints
 int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-			  const nsd_crec &rec, const uint32_t *ext_pool, const nsd_sll_t *sll)
+			  const nsd_crec &rec, uint32_t i, const uint32_t *ext_pool, const nsd_sll_t *sll)
 {
 	Out o(s);
 	Frame f{ pkt, caplen };
@@ -1109,6 +1109,17 @@ int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, i
 	uint32_t n = rec.nflags & 7u;
 	uint8_t ids[NSD_EXT_MAX_LAYERS];
 	uint16_t offs[NSD_EXT_MAX_LAYERS];
+	if (n == NSD_N_EXT && rec.nlayers) {
+		// 7..12 layers: ids 6.. in the packet's side word (pool word i)
+		if (!ext_pool || (rec.nflags & NSD_F_OVERFLOW) || rec.nlayers <= NSD_REC_MAX_LAYERS ||
+		    rec.nlayers > NSD_CREC_MAX_LAYERS)
+			return NSD_ERR_FORMAT;
+		n = rec.nlayers;
+		for (uint32_t k = 0; k < n; k++)
+			ids[k] = (uint8_t)(k < NSD_REC_MAX_LAYERS ? (rec.chain >> (5 * k)) & 31
+								  : (ext_pool[i] >> (5 * (k - NSD_REC_MAX_LAYERS))) & 31);
+		return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll);
+	}
 	if (n == NSD_N_EXT) {
 		if (ext_chain(ext_pool, rec.chain, rec.nflags, n, ids, offs) != NSD_OK)
 			return NSD_ERR_FORMAT;
@@ -1215,7 +1226,7 @@ extern "C" long nsd_format_batch_compact(const uint8_t *frames, const nsd_desc_t
 	for (uint32_t i = 0; i < n; i++) {
 		const uint64_t d = desc[i];
 		int r = nsd::format_packet_compact(s, frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), linktype, mode,
-						   crec[i], ext_pool, sll ? sll + i : nullptr);
+						   crec[i], i, ext_pool, sll ? sll + i : nullptr);
 		if (rc)
 			rc[i] = (int8_t)r;
 		if (ends)

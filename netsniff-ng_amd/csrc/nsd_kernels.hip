@@ -359,14 +359,18 @@ __device__ __forceinline__ void store_rec(uint4 *rec, uint32_t i, uint4 r)
 }
 
 // The record of packet i in the launch's record form: the 16-byte nsd_rec,
-// or (CR) the 8-byte nsd_crec {chain or ext slot, ip_csum, nflags} - the
-// same results without the cursors a renderer re-derives from the bytes
+// or (CR) the 8-byte nsd_crec - the same results without the cursors a
+// renderer re-derives from the bytes: the first 6 ids, the layer count in
+// nlayers for 7..12 layers (ids 6..11 in the packet's side word), or the ext
+// slot of a longer chain
 template <bool CR>
 __device__ __forceinline__ void put_rec(void *rec, uint32_t i, const WalkOut &w)
 {
 	if constexpr (CR) {
-		const uint32_t nf = (w.need_ext ? NSD_N_EXT : w.n) | w.flags;
-		const v2u v = { w.need_ext ? (w.ext_on ? w.slot : 0xFFFFFFFFu) : w.chain, w.ip_csum | nf << 16 };
+		const bool more = w.n > NSD_REC_MAX_LAYERS;
+		const uint32_t nf = (more ? NSD_N_EXT : w.n) | w.flags;
+		const uint32_t rs = more && !w.ext_on ? w.n : 0u;
+		const v2u v = { w.ext_on ? w.slot : w.chain, w.ip_csum | nf << 16 | rs << 24 };
 		__builtin_nontemporal_store(v, (v2u *)rec + i);
 	} else {
 		store_rec((uint4 *)rec, i, pack_record(w));
@@ -490,8 +494,11 @@ __device__ __forceinline__ uint64_t leaf_entry(uint32_t i, uint32_t start, int i
 // What a lane whose general walk ended leaves behind (wave-uniform call):
 // an ICMPv4 message past its windows and a host-rendered leaf go to the
 // wave's pending list, an ext chain to the pool (layers 0..5 from the record
-// registers, 6..15 from the wave's LDS list, deeper ones already in the
-// entry), then the record and the flag counts.
+// registers, 6..11 from the wave's LDS list, deeper ones already in the
+// entry), then the record and the flag counts.  Compact records keep a
+// chain of 7..12 layers in the packet's side word (ids 6..11, 5 bits each:
+// one coalesced 4-byte store instead of a pool entry, C4 -15 %); only
+// longer chains (entry taken at layer 12 by take_deep) write an entry.
 template <int MODE, bool CR>
 __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, uint32_t caplen, const GenSink &g,
 					     void *__restrict__ rec, Pending &pq, FlagCnt &fc, int lane)
@@ -511,13 +518,31 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 			wq[npend + lanes_below(pm)] = pend_entry(i, w.icmp_off, w.icmp_len);
 		npend += (uint32_t)__popcll(pm);
 	}
-	const bool ex = fin && w.need_ext;
+	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
+	static_assert(DEEP == NSD_CREC_MAX_LAYERS, "side words hold the LDS-listed layers");
+	if constexpr (CR) {
+		const bool sw = fin && w.n > NSD_REC_MAX_LAYERS && !w.ext_on;
+		if (__ballot(sw)) {
+			uint32_t word = 0;
+#pragma unroll
+			for (uint32_t j = NSD_REC_MAX_LAYERS; j < DEEP; j++)
+				word |= (j < w.n ? g.lay[(j - NSD_REC_MAX_LAYERS) * 64 + lane] & 31u : 0u)
+					<< (5 * (j - NSD_REC_MAX_LAYERS));
+			if (sw && g.side)
+				g.side[i] = word;
+			if (sw && !g.side)
+				w.flags |= NSD_F_OVERFLOW;   // no side words: the pool is smaller than the batch
+		}
+	}
+	const bool ex = fin && (CR ? w.ext_on : w.need_ext);
 	if (__ballot(ex)) {
 		const bool tk = ex && !w.ext_on;
-		const uint32_t sb = ext_take(g, tk, NSD_EXT_WORDS(NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS));
-		if (tk) {
-			w.slot = sb;
-			w.ext_on = true;
+		if (!CR) {
+			const uint32_t sb = ext_take(g, tk, NSD_EXT_WORDS(DEEP));
+			if (tk) {
+				w.slot = sb;
+				w.ext_on = true;
+			}
 		}
 		if (ex && w.slot == 0xFFFFFFFFu)
 			w.flags |= NSD_F_OVERFLOW;   // the pool is full
@@ -530,7 +555,6 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 				return j < nl ? g.lay[(j - NSD_REC_MAX_LAYERS) * 64 + lane] : 0u;
 			};
 			// layers 0 .. DEEP-1 (deeper ones are in the entry already)
-			constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
 			static_assert(DEEP % 4 == 0 && DEEP <= 16, "whole uint4 groups of a short entry");
 			*(uint4 *)e = make_uint4(i, nl, 0, 0);
 #pragma unroll
@@ -628,7 +652,11 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 
 	const uint32_t stride = gridDim.x * BLOCK;
 	uint64_t *const wq = pq.wq;
-	const GenSink g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, &sh.lay[wv][0] };
+	// compact records: pool words [0, n) are the packets' side words (when the
+	// pool has them), entries come after
+	const bool side = CR && ext_words >= n;
+	const GenSink g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, &sh.lay[wv][0],
+			 side ? n : 0u, side ? ext : nullptr };
 	FlagCnt fc;
 	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
 

@@ -97,6 +97,9 @@ struct GenSink {
 	uint32_t *wc;                 // LDS: this wave's chunk {next word, words left}
 	unsigned long long *s_cnt;    // LDS: block counters
 	uint32_t *lay;                // LDS: this wave's layer lists, [j * 64 + lane]
+	uint32_t sbase;               // first pool word handed out (compact records: the
+	                              // side words [0, n) come first)
+	uint32_t *side;               // compact records: side word of packet i (or null)
 
 	// wave-uniform branch condition: some lane needs the body
 	__device__ __forceinline__ bool any(bool c) const { return __ballot(c) != 0; }
@@ -134,8 +137,8 @@ __device__ __forceinline__ uint32_t ext_take(const GenSink &g, bool want, uint32
 		// a full pool takes no more chunks, so the counter cannot wrap round
 		// into it (the launcher caps pool_words well below 2^32)
 		if ((int)__lane_id() == leader &&
-		    __hip_atomic_load(g.used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g.pool_words)
-			b = atomicAdd(g.used, chunk);
+		    __hip_atomic_load(g.used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + g.sbase < g.pool_words)
+			b = atomicAdd(g.used, chunk) + g.sbase;
 		b = __shfl(b, leader, 64);
 		if (b == 0xFFFFFFFFu)
 			return 0xFFFFFFFFu;   // the wave's chunk state stays empty

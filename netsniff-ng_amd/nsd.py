@@ -25,7 +25,7 @@ REC_DTYPE = np.dtype([("chain", "<u4"), ("data_off", "<u2"), ("tail_off", "<u2")
                       ("ip_csum", "<u2"), ("nflags", "u1"), ("off2", "u1", (5,))])
 REC_BYTES = 16
 # nsd_crec: the compact 8-byte record (chain ids or ext slot, ip_csum, nflags)
-CREC_DTYPE = np.dtype([("chain", "<u4"), ("ip_csum", "<u2"), ("nflags", "u1"), ("rsvd", "u1")])
+CREC_DTYPE = np.dtype([("chain", "<u4"), ("ip_csum", "<u2"), ("nflags", "u1"), ("nlayers", "u1")])
 CREC_BYTES = 8
 
 # ext pool (include/netsniff_dissect.h "ext pool"): u32 words; an entry is a
@@ -274,16 +274,36 @@ def dissect_device_compact(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10
     return crec, ext, ext_used, counters
 
 
-def compact_of(rec):
-    """The compact records (CREC_DTYPE) that carry what 16-byte records do
-    minus the cursors: chain (or the ext slot), ip_csum, nflags."""
-    out = np.zeros(len(rec), dtype=CREC_DTYPE)
-    ext = (rec["nflags"] & 7) == 7
-    slots = rec["off2"][:, :4].copy().view("<u4").reshape(-1)
-    out["chain"] = np.where(ext, slots, rec["chain"])
+def compact_of(rec, ext=None):
+    """(crec, pool): the compact records (CREC_DTYPE) and their ext pool that
+    carry what 16-byte records `rec` with pool `ext` do, minus the cursors
+    (include/netsniff_dissect.h "compact records"): ids inline up to 6
+    layers, 7..12 layers with ids 6.. in the packet's side word (pool word
+    i), longer chains as entries (their slots moved past the n side words)."""
+    n = len(rec)
+    out = np.zeros(n, dtype=CREC_DTYPE)
+    side = np.zeros(n, dtype=np.uint32)
+    src = np.zeros(0, dtype=np.uint32) if ext is None else np.asarray(ext).view(np.uint32)
+    out["chain"] = rec["chain"]
     out["ip_csum"] = rec["ip_csum"]
     out["nflags"] = rec["nflags"]
-    return out
+    slots = rec["off2"][:, :4].copy().view("<u4").reshape(-1)
+    for i in np.nonzero((rec["nflags"] & 7) == 7)[0]:
+        s, flags = int(slots[i]), int(rec[i]["nflags"]) & 0xF8
+        if s == 0xFFFFFFFF:                  # no entry: pool full
+            out[i]["chain"] = s
+            continue
+        _, ids, _ = ext_entry(src, s)
+        if len(ids) > 12:
+            out[i]["chain"] = s + n
+            continue
+        out[i]["chain"] = sum(ids[k] << (5 * k) for k in range(min(len(ids), 6)))
+        if len(ids) <= 6:                    # ext form only for an offset past 510
+            out[i]["nflags"] = len(ids) | flags
+        else:
+            out[i]["nlayers"] = len(ids)
+            side[i] = sum(ids[k] << (5 * (k - 6)) for k in range(6, len(ids)))
+    return out, np.concatenate([side, src])
 
 
 def entry_batch(frames, desc, mode=PRINT_NORM, linktype=LINKTYPE_EN10MB, ext_words=None, sll=None):

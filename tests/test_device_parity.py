@@ -84,31 +84,35 @@ def test_synthetic_configs(cfg, n, mode):
 
 
 def _check_compact(frames, desc, mode):
-    """Compact device records == the oracle's records minus the cursors; ext
-    chains compared by their entries; counters equal."""
+    """Compact device records == the oracle's records minus the cursors
+    (nsd.compact_of): ids inline or in the side words, longer chains
+    compared by their entries; counters equal.  Returns (crec, pool)."""
     import torch
     f = torch.from_numpy(frames).cuda()
     d = torch.from_numpy(desc.view(np.int64)).cuda()
     crec, ext, used, cnt = nsd.dissect_device_compact(f, d, mode=mode)
     torch.cuda.synchronize()
+    n = len(desc)
     got = crec.cpu().numpy().view(nsd.CREC_DTYPE)
-    dext = ext.cpu().numpy().view(np.uint32)[:int(used.item())]
+    dpool = ext.cpu().numpy().view(np.uint32)[:n + int(used.item())]
     orec, oext, ocnt, _ = T.oracle_records(frames, desc, mode=mode)
-    want = nsd.compact_of(orec)
-    for fld in ("ip_csum", "nflags"):
+    want, wpool = nsd.compact_of(orec, oext)
+    for fld in ("ip_csum", "nflags", "nlayers"):
         bad = np.nonzero(got[fld] != want[fld])[0]
         assert len(bad) == 0, f"{fld} differs at {bad[:10]}"
-    inline = (want["nflags"] & 7) != 7
-    assert np.array_equal(got["chain"][inline], want["chain"][inline]), "chain ids differ"
-    for i in np.nonzero(~inline)[0]:
+    deep = ((want["nflags"] & 7) == 7) & (want["nlayers"] == 0)
+    assert np.array_equal(got["chain"][~deep], want["chain"][~deep]), "chain ids differ"
+    side = want["nlayers"] != 0
+    assert np.array_equal(dpool[:n][side], wpool[:n][side]), "side words differ"
+    for i in np.nonzero(deep)[0]:
         if want[i]["chain"] == 0xFFFFFFFF:      # no entry (pool full)
             assert got[i]["chain"] == 0xFFFFFFFF
             continue
-        gp, gids, goffs = nsd.ext_entry(dext, int(got[i]["chain"]))
-        _, oids, ooffs = nsd.ext_entry(oext, int(want[i]["chain"]))
+        gp, gids, goffs = nsd.ext_entry(dpool, int(got[i]["chain"]))
+        _, oids, ooffs = nsd.ext_entry(wpool, int(want[i]["chain"]))
         assert gp == i and (gids, goffs) == (oids, ooffs), f"ext chain differs at {i}"
     assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt)
-    return got, dext
+    return got, dpool
 
 
 @pytest.mark.parametrize("mode", MODES)

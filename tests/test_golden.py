@@ -125,8 +125,8 @@ def test_formatter_compact_matches_golden(name, mode):
     lt, pkts, frames, desc = batch(name)
     gold = load_golden(f"{name}.m{mode}.w65535")
     rec, ext, _, _ = T.oracle_records(frames, desc, linktype=lt, mode=mode)
-    crec = nsd.compact_of(rec)
-    texts, rc = nsd.format_batch_compact(frames, desc, crec, ext, mode=mode, linktype=lt)
+    crec, pool = nsd.compact_of(rec, ext)
+    texts, rc = nsd.format_batch_compact(frames, desc, crec, pool, mode=mode, linktype=lt)
     for i in range(len(pkts)):
         if rec[i]["nflags"] & 0x20:          # overflow: no chain in the record
             assert rc[i] != 0
@@ -143,7 +143,8 @@ def test_prefix_text_formatter_compact(key, cfg):
     frames, desc = T.make_batch(cfg, 65536)
     for m in (T.PRINT_NORM, T.PRINT_LESS):
         rec, ext, _, _ = T.oracle_records(frames, desc, mode=m)
-        texts, rc = nsd.format_batch_compact(frames, desc, nsd.compact_of(rec), ext, mode=m)
+        crec, pool = nsd.compact_of(rec, ext)
+        texts, rc = nsd.format_batch_compact(frames, desc, crec, pool, mode=m)
         assert (rc == 0).all()
         assert hashlib.sha256(b"".join(texts)).hexdigest() == want[f"{key}:m{m}"]["text_sha256"]
 

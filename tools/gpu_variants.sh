@@ -14,7 +14,7 @@ cp "$LIB" "$O/base.so"
 for v in $VARS; do
   if [ "$v" = base ]; then cp "$O/base.so" "$LIB"; else cp "$R/variants/$v/libnsdissect.so" "$LIB"; fi
   timeout -k 10 300 python -u tools/kbench.py --configs ${CFGS:-udp64,imix,ipv6x} --steps ${STEPS:-10} ${KB_ARGS} > "$O/$v.log" 2>&1; rc=$?
-  echo "== $v rc=$rc"; cat "$O/$v.log" | grep kernel_ms
+  echo "== $v rc=$rc"; grep -E "kernel_ms|phases" "$O/$v.log"
   [ $rc = 0 ] || { tail -5 "$O/$v.log"; cp "$O/base.so" "$LIB"; exit $rc; }
 done
 cp "$O/base.so" "$LIB"

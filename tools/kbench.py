@@ -41,6 +41,10 @@ def main():
             r = b.roofline(ms)
             print(f"{key:6s} rec{b.rec_b:<2d} kernel_ms={ms:.4f} frac={r['frac'] if r else None} "
                   f"read_frac={r['read_frac'] if r else None} pkts_counted={int(cnt[32])}", flush=True)
+            if os.environ.get("KB_PHASES"):
+                # counters 48..55 of an instrumented variant (tools/variants/phases.patch):
+                # per-wave clock sums of the last launch
+                print(f"{key:6s} phases {[int(x) for x in cnt[48:56]]}", flush=True)
             b.free()
             torch.cuda.empty_cache()
 
