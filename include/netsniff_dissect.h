@@ -402,7 +402,7 @@ int nsd_walk_packet_cpu(const uint8_t *pkt, uint32_t caplen, int linktype, int m
  *    NSD_F_OVERFLOW); pool entries start at word n + *d_ext_used;
  *  - longer chains: chain = the ext pool slot (0xFFFFFFFF with
  *    NSD_F_OVERFLOW: pool full), nflags & 7 = NSD_N_EXT, nlayers = 0; the
- *    entry keeps ids and layer offsets.
+ *    entry keeps the ids (offset bits 0: no cursors in this form either).
  * nflags (besides the count), ip_csum: as in nsd_rec.  The counters are the
  * same as for 16-byte records (NSD_CNT_EXT counts the chains that need the
  * 16-byte record's ext form). */
@@ -422,8 +422,7 @@ int nsd_dissect_device_compact(const uint8_t *d_frames, const nsd_desc_t *d_desc
 			       uint32_t *d_ext_used, uint64_t *d_counters, void *d_workspace,
 			       void *stream);
 /* nsd_format_batch_sll over compact records: each layer starts where the
- * previous one's print left the cursor; an ext chain is also checked
- * against its entry's offsets.  A record without its chain (NSD_F_OVERFLOW)
+ * previous one's print left the cursor.  A record without its chain (NSD_F_OVERFLOW)
  * gets rc NSD_ERR_FORMAT (render it per packet: dissector_entry_point). */
 long nsd_format_batch_compact(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
 			      uint32_t n, int linktype, int mode, const nsd_crec *crec,

@@ -1121,9 +1121,10 @@ int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, i
 		return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll);
 	}
 	if (n == NSD_N_EXT) {
+		// (a compact chain's entry holds ids only)
 		if (ext_chain(ext_pool, rec.chain, rec.nflags, n, ids, offs) != NSD_OK)
 			return NSD_ERR_FORMAT;
-		return format_chain(o, f, linktype, mode, n, ids, offs, nullptr, rec.ip_csum, rec.nflags, sll);
+		return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll);
 	}
 	for (uint32_t k = 0; k < n; k++)
 		ids[k] = (uint8_t)((rec.chain >> (5 * k)) & 31);

@@ -497,10 +497,11 @@ __device__ __forceinline__ uint64_t leaf_entry(uint32_t i, uint32_t start, int i
 // registers, 6..11 from the wave's LDS list, deeper ones already in the
 // entry), then the record and the flag counts.  Compact records keep a
 // chain of 7..12 layers in the packet's side word (ids 6..11, 5 bits each:
-// one coalesced 4-byte store instead of a pool entry, C4 -15 %); only
-// longer chains (entry taken at layer 12 by take_deep) write an entry.
+// one coalesced 4-byte store instead of a pool entry, C4 -25 %); only
+// longer chains (entry taken at layer 12 by take_deep) write an entry, with
+// ids only.
 template <int MODE, bool CR>
-__device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, uint32_t caplen, const GenSink &g,
+__device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, uint32_t caplen, const GenSink<CR> &g,
 					     void *__restrict__ rec, Pending &pq, FlagCnt &fc, int lane)
 {
 	// (the compact record has no cursor for the leaf pass to set)
@@ -522,17 +523,10 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 	static_assert(DEEP == NSD_CREC_MAX_LAYERS, "side words hold the LDS-listed layers");
 	if constexpr (CR) {
 		const bool sw = fin && w.n > NSD_REC_MAX_LAYERS && !w.ext_on;
-		if (__ballot(sw)) {
-			uint32_t word = 0;
-#pragma unroll
-			for (uint32_t j = NSD_REC_MAX_LAYERS; j < DEEP; j++)
-				word |= (j < w.n ? g.lay[(j - NSD_REC_MAX_LAYERS) * 64 + lane] & 31u : 0u)
-					<< (5 * (j - NSD_REC_MAX_LAYERS));
-			if (sw && g.side)
-				g.side[i] = word;
-			if (sw && !g.side)
-				w.flags |= NSD_F_OVERFLOW;   // no side words: the pool is smaller than the batch
-		}
+		if (sw && g.side)
+			g.side[i] = w.offB;
+		if (sw && !g.side)
+			w.flags |= NSD_F_OVERFLOW;   // no side words: the pool is smaller than the batch
 	}
 	const bool ex = fin && (CR ? w.ext_on : w.need_ext);
 	if (__ballot(ex)) {
@@ -550,6 +544,9 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 			uint32_t *e = g.pool + w.slot;
 			const uint32_t nl = w.n < NSD_EXT_MAX_LAYERS ? w.n : NSD_EXT_MAX_LAYERS;
 			auto lv = [&](uint32_t j) -> uint32_t {
+				if (CR)   // ids only
+					return j < NSD_REC_MAX_LAYERS ? (w.chain >> (5 * j)) & 31
+								      : (w.offB >> (5 * (j - NSD_REC_MAX_LAYERS))) & 31;
 				if (j < NSD_REC_MAX_LAYERS)
 					return ((w.chain >> (5 * j)) & 31) | (uint32_t)off_of(w, j) << 16;
 				return j < nl ? g.lay[(j - NSD_REC_MAX_LAYERS) * 64 + lane] : 0u;
@@ -585,7 +582,7 @@ template <int MODE, bool CR>
 __device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restrict__ frames, uint64_t d,
 					      uint32_t i, uint32_t fw, WalkOut &w, int start_id,
 					      const uint32_t *__restrict__ sll, void *__restrict__ rec,
-					      const GenSink &g, Pending &pq, FlagCnt &fc)
+					      const GenSink<CR> &g, Pending &pq, FlagCnt &fc)
 {
 	constexpr int ROW = WIN2 / 4;
 	const int lane = threadIdx.x & 63;
@@ -655,7 +652,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	// compact records: pool words [0, n) are the packets' side words (when the
 	// pool has them), entries come after
 	const bool side = CR && ext_words >= n;
-	const GenSink g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, &sh.lay[wv][0],
+	const GenSink<CR> g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, &sh.lay[wv][0],
 			 side ? n : 0u, side ? ext : nullptr };
 	FlagCnt fc;
 	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate

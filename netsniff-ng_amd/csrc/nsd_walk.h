@@ -71,7 +71,8 @@ struct WalkOut {
 	uint32_t n;          // layers run
 	uint32_t chain;      // first 6 ids, 5 bits each
 	uint64_t offA;       // offsets of layers 0..3 (16 bits each)
-	uint32_t offB;       // offsets of layers 4..5
+	uint32_t offB;       // offsets of layers 4..5; compact records (no offsets):
+	                     // ids 6..11, 5 bits each (the side word)
 	uint16_t ip_csum;
 	uint8_t  flags;      // NSD_F_*
 	bool     need_ext;   // more than 6 layers or a layer start > 510
@@ -83,13 +84,18 @@ struct WalkOut {
 	int      leaf;       // device: a host-rendered leaf at w.data whose end is still to walk
 };
 
-// Where the general walk puts what it records beyond the 16-byte record:
-// layers 6 .. 6+NSD_LDS_LAYERS-1 in a per-lane LDS list (written out with the
-// packet's pool entry when its walk ends), deeper layers straight into the
-// packet's pool entry (taken when the chain reaches that depth).  Pool words
-// come from per-wave chunks (ext_take).
+// Where the general walk puts what it records beyond the record's 6 layers:
+// 16-byte records (CR false) keep layers 6 .. 6+NSD_LDS_LAYERS-1 (id and
+// start) in a per-lane LDS list, written out with the packet's pool entry
+// when its walk ends; compact records (CR) keep no layer starts at all (the
+// renderer re-derives them), so their ids 6..11 stay in a register
+// (offB, free in that form: the side word).  Deeper layers go straight into the packet's pool
+// entry (taken when the chain reaches that depth).  Pool words come from
+// per-wave chunks (ext_take).
 #define NSD_LDS_LAYERS 6
+template <bool CR>
 struct GenSink {
+	static constexpr bool OFFS = !CR;   // the walk tracks layer starts
 	uint32_t *pool;               // the ext pool
 	uint32_t pool_words;
 	uint32_t *used;               // pool words handed out (global)
@@ -121,7 +127,8 @@ struct GenSink {
 // chunk is taken with one global atomic when the current one is short (its
 // tail is left unused).  Returns the entry's word index, or 0xFFFFFFFF when
 // it does not fit in the pool (or !want).
-__device__ __forceinline__ uint32_t ext_take(const GenSink &g, bool want, uint32_t words)
+template <class G>
+__device__ __forceinline__ uint32_t ext_take(const G &g, bool want, uint32_t words)
 {
 	const uint64_t m = __ballot(want);
 	if (!m)
@@ -154,20 +161,23 @@ __device__ __forceinline__ uint32_t ext_take(const GenSink &g, bool want, uint32
 	return want && (uint64_t)s + words <= g.pool_words ? s : 0xFFFFFFFFu;
 }
 
-// the sink's layer store: layers 6..15 in the wave's LDS list, deeper ones in
-// the packet's pool entry (taken by take_deep)
-__device__ __forceinline__ void GenSink::layer(const WalkOut &w, uint32_t k, int id, uint32_t start) const
+// the sink's layer store: (16-byte records) layers 6..11 in the wave's LDS
+// list, deeper ones in the packet's pool entry (taken by take_deep);
+// compact records store only the deeper ones' ids
+template <bool CR>
+__device__ __forceinline__ void GenSink<CR>::layer(const WalkOut &w, uint32_t k, int id, uint32_t start) const
 {
 	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
 	atomicAdd(&s_cnt[NSD_CNT_OPS + id], 1ull);   // the oracle counts the first 64 layers
-	const uint32_t lv = (uint32_t)id | start << 16;
-	if (k >= NSD_REC_MAX_LAYERS && k < DEEP)
+	const uint32_t lv = CR ? (uint32_t)id : (uint32_t)id | start << 16;
+	if (!CR && k >= NSD_REC_MAX_LAYERS && k < DEEP)
 		lay[(k - NSD_REC_MAX_LAYERS) * 64 + __lane_id()] = lv;
 	else if (k >= DEEP && w.slot != 0xFFFFFFFFu)
 		pool[w.slot + NSD_EXT_HDR_WORDS + k] = lv;
 }
 
-__device__ __forceinline__ void GenSink::take_deep(bool deep_first, WalkOut &w) const
+template <bool CR>
+__device__ __forceinline__ void GenSink<CR>::take_deep(bool deep_first, WalkOut &w) const
 {
 	if (__ballot(deep_first)) {
 		// room for every layer the record may hold (the chain's length is not
@@ -183,6 +193,7 @@ __device__ __forceinline__ void GenSink::take_deep(bool deep_first, WalkOut &w) 
 // The host walk's sink: every layer into the caller's arrays (the host
 // keeps the whole chain, so nothing is taken from a pool while walking)
 struct HostSink {
+	static constexpr bool OFFS = true;
 	uint8_t *ids;                 // [NSD_EXT_MAX_LAYERS]
 	uint16_t *offs;               // [NSD_EXT_MAX_LAYERS]
 	uint64_t *counters;           // NSD_NCOUNTERS, or NULL
@@ -375,8 +386,13 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	const uint32_t kk = k < 8 ? k : 7;   // keeps the shifts below defined
 	w.need_ext = w.need_ext || need_now;
 	w.chain |= act && k < NSD_REC_MAX_LAYERS ? (uint32_t)id << (5 * kk) : 0u;
-	w.offA |= act && k < 4 ? (uint64_t)(start & 0xFFFF) << (16 * (kk & 3)) : 0ull;
-	w.offB |= act && k >= 4 && k < NSD_REC_MAX_LAYERS ? (start & 0xFFFF) << (16 * (kk & 1)) : 0u;
+	if constexpr (Sink::OFFS) {
+		w.offA |= act && k < 4 ? (uint64_t)(start & 0xFFFF) << (16 * (kk & 3)) : 0ull;
+		w.offB |= act && k >= 4 && k < NSD_REC_MAX_LAYERS ? (start & 0xFFFF) << (16 * (kk & 1)) : 0u;
+	} else {
+		w.offB |= act && k >= NSD_REC_MAX_LAYERS && k < DEEP
+				    ? (uint32_t)id << (5 * ((k - NSD_REC_MAX_LAYERS) & 7)) : 0u;
+	}
 	w.flags |= act && k >= NSD_EXT_MAX_LAYERS ? NSD_F_OVERFLOW : 0;
 	if (act && k < NSD_EXT_MAX_LAYERS)
 		g.layer(w, k, id, start);
