@@ -21,9 +21,10 @@
 // The fast walk finishes every packet whose chain resolves inside its first
 // 64 bytes, with the next tile's chunks and the tile after next's descriptors
 // in flight while the current tile is walked from LDS only.  The tile's
-// other lanes continue at once with the general walk (continue_walk):
-// per-lane window restaging at each lane's cursor, ext spill; ICMPv4 payload
-// checksums longer than a window are summed by the block at the end.
+// other packets go to the wave's walkers, the general walk (walkers):
+// per-lane windows staged at each walker's cursor, idle walkers refilled,
+// ext spill; ICMPv4 payload checksums longer than a window are summed by the
+// block at the end.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -458,6 +459,7 @@ struct Shared {
 	uint32_t wc[WAVES][2];                      // per-wave ext pool chunk {next word, words left}
 	uint32_t pcnt[WAVES];                       // pending checksums per wave
 	uint32_t lay[WAVES][NSD_LDS_LAYERS * 64];   // general-walk layer lists (layers 6..15)
+	uint8_t tmap[WAVES][64];                    // take(): pending lane of each rank
 };
 
 // The LINKTYPE_LINUX_SLL head (dissector_sll.c:39-82): pulls nothing; in
@@ -565,74 +567,141 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 	fc.add(w, caplen, fin);
 }
 
-// The lanes of a tile the fast walk could not finish inside their first 64
-// bytes, walked on at once by the general walk (gen_step): from where the
-// fast walk stopped (FW_RESUME: Ethernet, tags and the IP header recorded)
-// or from the start (FW_RESTART: other link types, MPLS, deeper tag stacks,
-// bytes past the first window).  A round stages each such lane's WIN2-byte
-// window at its cursor - the lines the fast walk has just read are still in
-// L2, the next ones are read once, 4 consecutive lanes per 64 bytes of a
-// window (coalesced) - and runs layers until the lane's chain ends or needs
-// bytes past the window; the wave repeats rounds until all its lanes are
-// done.  Measured alternatives (C4): a separate pass over queued
-// packets (the lines were evicted by then), per-step loads straight from
-// L2 (64 lines per wave instruction: the vector-memory address path, not the
-// bytes, bound it).
+// The general walk's pool: every lane of a wave is also a walker that holds
+// (at most) one packet the fast walk could not finish.  A tile's deferred
+// packets are handed to free walkers in lane order; a session stages the
+// windows of the walkers that need one (new, or suspended at the end of
+// their window) and steps every walker that can step.  While packets are
+// still waiting for a walker, a session stops as soon as NSD_REFILL walkers
+// are idle, to take them; the tile's last session runs until every walker
+// is done or suspended, and the suspended ones are carried to the next
+// tile's session (their next window would be restaged anyway).  So a tile
+// costs one window wait (1.15 sessions per C4 tile against 2 rounds) and
+// its steps run with refilled lanes (7.2 layer steps per C4 tile against 9.8
+// when each tile's deferred lanes are walked to their ends).
+#ifndef NSD_REFILL
+#define NSD_REFILL 16   // idle walkers at which a session stops to take waiting packets
+#endif
+struct Walker {
+	WalkOut w;
+	uint64_t d;       // its packet's descriptor
+	uint32_t i;       // its packet's index
+	uint32_t wb;      // aligned position of its staged window
+	bool have;        // holds a packet
+	bool stage;       // its window must be (re)staged before it steps again
+};
+
+// Hand the waiting packets (lanes with pnd: the tile's deferred packets, walk
+// state pw after walk_init / the fast walk's layers) to free walkers: the
+// waiting lane of rank r goes to the free walker of rank r (a lane map in
+// LDS, then one shuffle per state word).
+template <bool CR>
+__device__ __forceinline__ void take(Shared &sh, Walker &wk, bool &pnd, const WalkOut &pw, uint32_t pi, uint64_t pd,
+				     int lane, int wv);
+
 template <int MODE, bool CR>
-__device__ __forceinline__ void continue_walk(Shared &sh, const uint8_t *__restrict__ frames, uint64_t d,
-					      uint32_t i, uint32_t fw, WalkOut &w, int start_id,
-					      const uint32_t *__restrict__ sll, void *__restrict__ rec,
-					      const GenSink<CR> &g, Pending &pq, FlagCnt &fc)
+__device__ __forceinline__ void walkers(Shared &sh, const uint8_t *__restrict__ frames, void *__restrict__ rec,
+					const GenSink<CR> &g, Pending &pq, FlagCnt &fc, Walker &wk, bool &pnd,
+					const WalkOut &pw, uint32_t pi, uint64_t pd, bool drain)
 {
 	constexpr int ROW = WIN2 / 4;
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
-	const bool on = fw != FW_DONE;
-	const uint32_t caplen = NSD_DESC_CAPLEN(d), m = (uint32_t)NSD_DESC_OFF(d) & 15;
-	if (on) {
-		if (fw == FW_RESTART) {
-			walk_init(w, caplen, start_id);
-			if (start_id == NSD_OPS_SLL)
-				sll_head<MODE>(sh, w, sll, i);
-		} else {
-			// the layers the fast walk ran (its finished chains are counted
-			// by chain word; these are counted here)
-			for (uint32_t k = 0; k < w.n; k++)
-				atomicAdd(&sh.cnt[NSD_CNT_OPS + ((w.chain >> (5 * k)) & 31)], 1ull);
+	for (;;) {
+		take<CR>(sh, wk, pnd, pw, pi, pd, lane, wv);
+		if (!__ballot(wk.have))
+			break;
+		const bool more = __ballot(pnd) != 0;
+		// ---- a session
+		const uint64_t off = NSD_DESC_OFF(wk.d);
+		const uint32_t caplen = NSD_DESC_CAPLEN(wk.d), m = (uint32_t)off & 15;
+		const bool st = wk.have && wk.stage;
+		if (st)
+			wk.wb = (wk.w.data + m) & ~15u;
+		if (__ballot(st)) {
+			// (the window's HBM address and extent are recomputed from the
+			// descriptor rather than kept live across the walk: registers)
+			const uint32_t lim = caplen + m;   // first aligned position past the frame
+			stage_glds<WIN2>(&sh.win[wv][0], (uint64_t)(frames + (off & ~15ull)) + wk.wb,
+					 st && wk.wb < lim ? lim - wk.wb : 0u, lane);
 		}
-	}
-	bool have = on;
-	uint32_t wb = (w.data + m) & ~15u;
-	while (__ballot(have)) {
-		// (the window's address and extent are recomputed per round from the
-		// descriptor rather than kept live across the walk: registers)
-		const uint32_t lim = caplen + m;   // first aligned position past the frame
-		stage_glds<WIN2>(&sh.win[wv][0], (uint64_t)(frames + (NSD_DESC_OFF(d) & ~15ull)) + wb,
-				 have && wb < lim ? lim - wb : 0u, lane);
-		const LSrc<false, WIN2> src{ &sh.win[wv][lane * ROW], sh.lay3, sh.step, frames + NSD_DESC_OFF(d),
-					     caplen, m, wb, false, swz_of((uint32_t)lane, WIN2 / 16) << 2 };
+		const LSrc<false, WIN2> src{ &sh.win[wv][lane * ROW], sh.lay3, sh.step, frames + off,
+					     caplen, m, wk.wb, false, swz_of((uint32_t)lane, WIN2 / 16) << 2 };
 		bool susp;
 		for (;;) {
-			const bool run = have && w.id != 0;
-			susp = run && src.near_end(w.data, w.id);
+			const bool run = wk.have && wk.w.id != 0;
+			susp = run && src.near_end(wk.w.data, wk.w.id);
 			const bool act = run && !susp;
-			if (!__ballot(act))
+			const uint64_t am = __ballot(act);
+			if (!am)
 				break;
-			gen_step<MODE>(src, act, w, g);
+			if (more && __popcll(am) <= 64 - NSD_REFILL)
+				break;   // enough idle walkers: take waiting packets
+			gen_step<MODE>(src, act, wk.w, g);
 		}
 		wave_sync_lds();
-		emit_general<MODE, CR>(have && !susp, w, i, caplen, g, rec, pq, fc, lane);
-		have = have && susp;
-		if (susp)
-			wb = (w.data + m) & ~15u;
+		const bool fin = wk.have && wk.w.id == 0;
+		emit_general<MODE, CR>(fin, wk.w, wk.i, caplen, g, rec, pq, fc, lane);
+		wk.have = wk.have && !fin;
+		wk.stage = susp;
+		if (!drain && !more)
+			break;   // every walker is done or suspended: the next tile
 	}
+}
+
+template <bool CR>
+__device__ __forceinline__ void take(Shared &sh, Walker &wk, bool &pnd, const WalkOut &pw, uint32_t pi, uint64_t pd,
+				     int lane, int wv)
+{
+	const uint64_t P = __ballot(pnd), F = __ballot(!wk.have);
+	if (!P || !F)
+		return;
+	const uint32_t rp = lanes_below(P), rf = lanes_below(F);
+	const uint32_t np = (uint32_t)__popcll(P), nf = (uint32_t)__popcll(F);
+	if (pnd && rp < nf)
+		sh.tmap[wv][rp] = (uint8_t)lane;
+	wave_sync_lds();
+	const bool get = !wk.have && rf < np;
+	const int src = get ? (int)sh.tmap[wv][rf] : lane;
+	const uint32_t x0 = __shfl(pi, src, 64);
+	const uint32_t x1 = __shfl((uint32_t)pd, src, 64);
+	const uint32_t x2 = __shfl((uint32_t)(pd >> 32), src, 64);
+	const uint32_t x3 = __shfl(pw.data | pw.tail << 16, src, 64);
+	// (a deferred chain has at most 4 layers: Ethernet, 2 tags, IP)
+	const uint32_t x4 = __shfl((uint32_t)pw.ip_csum | (uint32_t)pw.flags << 16 | pw.n << 24 | (uint32_t)pw.id << 27,
+				   src, 64);
+	const uint32_t x5 = __shfl(pw.chain, src, 64);
+	uint32_t x6 = 0, x7 = 0, x8 = 0;
+	if (!CR) {
+		x6 = __shfl((uint32_t)pw.offA, src, 64);
+		x7 = __shfl((uint32_t)(pw.offA >> 32), src, 64);
+		x8 = __shfl(pw.offB, src, 64);
+	}
+	if (get) {
+		wk.i = x0;
+		wk.d = x1 | (uint64_t)x2 << 32;
+		walk_init(wk.w, x3 >> 16, (int)(x4 >> 27));
+		wk.w.data = x3 & 0xFFFF;
+		wk.w.ip_csum = (uint16_t)x4;
+		wk.w.flags = (uint8_t)(x4 >> 16);
+		wk.w.n = (x4 >> 24) & 7;
+		wk.w.chain = x5;
+		if (!CR) {
+			wk.w.offA = x6 | (uint64_t)x7 << 32;
+			wk.w.offB = x8;
+		}
+	}
+	wk.have = wk.have || get;
+	wk.stage = wk.stage || get;
+	pnd = pnd && rp >= nf;
 }
 
 // ---- the walk ------------------------------------------------------------------
 // Every packet of the block's grid-stride tiles, one wave per 64-packet tile:
-// the fast walk over each packet's first 64 bytes, then the general walk
-// for the lanes it could not finish (continue_walk); ICMPv4 messages past
-// the windows and host-rendered leaves go to the wave's pending list (pq).
+// the fast walk over each packet's first 64 bytes, then the general walk's
+// walkers take the packets it could not finish (walkers); ICMPv4 messages
+// past the windows and host-rendered leaves go to the wave's pending list
+// (pq).
 template <int MODE, bool CR>
 __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict__ frames,
 					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
@@ -683,78 +752,111 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	uint64_t d1 = (base + stride < n && base + stride + lane < n) ? desc[base + stride + lane] : 0;
 	Chunks<WIN1> ch;
 	stage_load<WIN1>(ch, frames, d0, lane);
+	Walker wk;
+	walk_init(wk.w, 0, 0);
+	wk.d = 0;
+	wk.i = 0;
+	wk.wb = 0;
+	wk.have = false;
+	wk.stage = false;
 
-	for (; base < n; base += stride) {
+	// (one more pass after the last tile drains the walkers: the engine is
+	// inlined once)
+	for (;; base += stride) {
+		const bool last = base >= n;
 		const uint32_t i = base + lane;
 		const bool valid = i < n;
 		const uint64_t off = NSD_DESC_OFF(d0);
 		const uint32_t caplen = NSD_DESC_CAPLEN(d0);
-
-		stage_write(&s_win[wv][0], ch, lane);
-		// prefetch: descriptors of tile t+2, chunks of tile t+1
-		const uint32_t b2 = base + 2 * stride;
-		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
-		const uint32_t b1 = base + stride;
-		if (b1 < n)
-			stage_load<WIN1>(ch, frames, d1, lane);
-		wave_sync_lds();
-
 		WalkOut w;
 		walk_init(w, caplen, valid ? start_id : 0);
-		uint32_t fw = FW_DONE;
-		if (valid) {
-			const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
-						    (uint32_t)off & 15, 0, false };
-			fw = fast_walk<MODE>(src, caplen, w);
-		}
-		const bool deferred = fw != FW_DONE;
-		wave_sync_lds();
-		const bool done = valid && !deferred;
-		if (MODE == PRINT_NORM) {
-			// ICMPv4 messages past the window: listed for the checksum pass, which
-			// patches the record if the sum is bad
-			const bool pnd = w.icmp_pend && done;
-			const uint64_t pmask = __ballot(pnd);
-			if (pnd)
-				wq[pq.npend + lanes_below(pmask)] = pend_entry(i, w.icmp_off, w.icmp_len);
-			pq.npend += (uint32_t)__popcll(pmask);
-		}
-		// per-ops counts from the finished chains, grouped by chain word
-		// (ids are >= 1, so equal chain words imply equal layer counts) for
-		// the first two distinct chains of the tile (C2: one), the rest per
-		// lane (C3: -4.5 % against looping over every distinct chain)
-		{
-			uint32_t key = done ? w.chain : 0xFFFFFFFFu;
-			for (int it = 0;; it++) {
-				const uint64_t pm = __ballot(key != 0xFFFFFFFFu);
-				if (!pm)
-					break;
-				if (it == 2) {
-					// more than two distinct chains in the tile: the rest
-					// count their own layers (the LDS serialises them)
-					if (key != 0xFFFFFFFFu)
-						for (uint32_t k = 0; k < w.n; k++)
-							atomicAdd(&s_cnt[NSD_CNT_OPS + ((key >> (5 * k)) & 31)], 1ull);
-					break;
+		bool deferred = false;
+		uint64_t d2 = 0;
+		if (!last) {
+			stage_write(&s_win[wv][0], ch, lane);
+			// prefetch: descriptors of tile t+2, chunks of tile t+1
+			const uint32_t b2 = base + 2 * stride;
+			d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
+			const uint32_t b1 = base + stride;
+			if (b1 < n)
+				stage_load<WIN1>(ch, frames, d1, lane);
+			wave_sync_lds();
+
+			uint32_t fw = FW_DONE;
+			if (valid) {
+				const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
+							    (uint32_t)off & 15, 0, false };
+				fw = fast_walk<MODE>(src, caplen, w);
+			}
+			deferred = fw != FW_DONE;
+			wave_sync_lds();
+			const bool done = valid && !deferred;
+			if (MODE == PRINT_NORM) {
+				// ICMPv4 messages past the window: listed for the checksum pass, which
+				// patches the record if the sum is bad
+				const bool pnd = w.icmp_pend && done;
+				const uint64_t pmask = __ballot(pnd);
+				if (pnd)
+					wq[pq.npend + lanes_below(pmask)] = pend_entry(i, w.icmp_off, w.icmp_len);
+				pq.npend += (uint32_t)__popcll(pmask);
+			}
+			// per-ops counts from the finished chains, grouped by chain word
+			// (ids are >= 1, so equal chain words imply equal layer counts) for
+			// the first two distinct chains of the tile (C2: one), the rest per
+			// lane (C3: -4.5 % against looping over every distinct chain)
+			{
+				uint32_t key = done ? w.chain : 0xFFFFFFFFu;
+				for (int it = 0;; it++) {
+					const uint64_t pm = __ballot(key != 0xFFFFFFFFu);
+					if (!pm)
+						break;
+					if (it == 2) {
+						// more than two distinct chains in the tile: the rest
+						// count their own layers (the LDS serialises them)
+						if (key != 0xFFFFFFFFu)
+							for (uint32_t k = 0; k < w.n; k++)
+								atomicAdd(&s_cnt[NSD_CNT_OPS + ((key >> (5 * k)) & 31)], 1ull);
+						break;
+					}
+					const int leader = __ffsll((unsigned long long)pm) - 1;
+					const uint32_t lk = __shfl(key, leader, 64);
+					const uint64_t m = __ballot(key == lk);
+					if (lane == leader) {
+						const uint32_t cnt = (uint32_t)__popcll(m);
+						for (uint32_t k = 0, nl = w.n; k < nl; k++)
+							atomicAdd(&s_cnt[NSD_CNT_OPS + ((lk >> (5 * k)) & 31)],
+								  (unsigned long long)cnt);
+					}
+					if (key == lk)
+						key = 0xFFFFFFFFu;
 				}
-				const int leader = __ffsll((unsigned long long)pm) - 1;
-				const uint32_t lk = __shfl(key, leader, 64);
-				const uint64_t m = __ballot(key == lk);
-				if (lane == leader) {
-					const uint32_t cnt = (uint32_t)__popcll(m);
-					for (uint32_t k = 0, nl = w.n; k < nl; k++)
-						atomicAdd(&s_cnt[NSD_CNT_OPS + ((lk >> (5 * k)) & 31)],
-							  (unsigned long long)cnt);
+			}
+			if (done)
+				put_rec<CR>(rec, i, w);
+			fc.add(w, caplen, done);
+			// the deferred packets' walk state for the general walk: from the
+			// start (FW_RESTART: other link types, MPLS, deeper tag stacks, bytes
+			// past the first window) or from where the fast walk stopped
+			// (FW_RESUME: its layers recorded; its finished chains are counted by
+			// chain word, these are counted here)
+			if (deferred) {
+				if (fw == FW_RESTART) {
+					walk_init(w, caplen, start_id);
+					if (start_id == NSD_OPS_SLL)
+						sll_head<MODE>(sh, w, sll, i);
+				} else {
+					for (uint32_t k = 0; k < w.n; k++)
+						atomicAdd(&s_cnt[NSD_CNT_OPS + ((w.chain >> (5 * k)) & 31)], 1ull);
 				}
-				if (key == lk)
-					key = 0xFFFFFFFFu;
 			}
 		}
-		if (done)
-			put_rec<CR>(rec, i, w);
-		fc.add(w, caplen, done);
-		if (__ballot(deferred))
-			continue_walk<MODE, CR>(sh, frames, d0, i, fw, w, start_id, sll, rec, g, pq, fc);
+		// (the walkers carried over are suspended: their windows are
+		// restaged anyway, so this tile's staging may reuse their rows)
+		bool pnd = deferred;
+		if (__ballot(pnd || wk.have))
+			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, pnd, w, i, d0, last);
+		if (last)
+			break;
 		d0 = d1;
 		d1 = d2;
 	}
