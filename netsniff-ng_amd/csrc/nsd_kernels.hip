@@ -47,6 +47,9 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #ifndef NSD_MINW
 #define NSD_MINW 4                 // waves per SIMD the fused kernel is register-allocated for
 #endif
+#ifndef NSD_L2PF
+#define NSD_L2PF 16                // a tile with this many deferred packets touches tile t+2's lines
+#endif
 #ifndef NSD_CSUM_SPLIT
 #define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
 #endif
@@ -297,6 +300,22 @@ __device__ __forceinline__ void stage_glds(uint32_t *wwin, uint64_t abase, uint3
 	}
 	// the DMA's LDS writes are ordered for this wave's reads by its vmcnt only
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Touch the first line(s) of a packet's fast window so a later load of it
+// hits L2: one 4-byte LDS-DMA load per line (64 lanes write 256 bytes of
+// `dummy`, an LDS area nothing reads, so no VGPR waits for the line).  Both
+// lines when the window straddles a 128-byte line.
+__device__ __forceinline__ void l2_touch(const uint8_t *frames, uint64_t d, uint32_t *dummy, bool on)
+{
+	const uint64_t a = (uint64_t)frames + NSD_DESC_OFF(d);
+	const uint32_t span = NSD_DESC_CAPLEN(d) < 64 ? (uint32_t)NSD_DESC_CAPLEN(d) : 64u;
+	if (on)
+		__builtin_amdgcn_global_load_lds((const void *)(a & ~127ull),
+						 (__attribute__((address_space(3))) void *)dummy, 4, 0, 0);
+	if (on && (a & 127) + span > 128)
+		__builtin_amdgcn_global_load_lds((const void *)((a & ~127ull) + 128),
+						 (__attribute__((address_space(3))) void *)dummy, 4, 0, 0);
 }
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -853,10 +872,23 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 		// (the walkers carried over are suspended: their windows are
 		// restaged anyway, so this tile's staging may reuse their rows)
 		bool pnd = deferred;
+		const bool many = __popcll(__ballot(pnd)) >= NSD_L2PF;
 		if (__ballot(pnd || wk.have))
 			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, pnd, w, i, d0, last);
 		if (last)
 			break;
+		// While the walkers are busy (C4), the lines of tile t+2 go into L2
+		// now, so the next iteration's loads of them wait for L2 rather than
+		// HBM: the walkers' first window wait (s_waitcnt vmcnt(0)) also
+		// waits for those loads (C4 1.45 -> 1.32 ms).  Not for tiles the
+		// fast walk finishes (C2, C3): there the next loads would wait for
+		// the touches (vector memory counts in order; C2 +12 %).  The
+		// LDS-DMA target is window words past the fast rows.
+		{
+			const uint32_t b2 = base + 2 * stride;
+			if (many && b2 < n)
+				l2_touch(frames, d2, &s_win[wv][64 * ROW], b2 + lane < n);
+		}
 		d0 = d1;
 		d1 = d2;
 	}
