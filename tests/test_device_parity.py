@@ -276,3 +276,55 @@ def _icmp_sweep(seed=7):
 def test_icmp_checksum_sweep(align):
     frames, desc = T.batch_from_packets(_icmp_sweep(), align=align)
     _check(frames, desc, T.PRINT_NORM)
+
+
+def _packets_of(frames, desc):
+    offs, caps = T.desc_off(desc), T.desc_caplen(desc)
+    return [bytes(frames[o:o + c]) for o, c in zip(offs, caps)]
+
+
+def _mixed_tiles(seed=5):
+    """64-packet tiles of different kinds in a fixed order: C4 tiles (nearly
+    every packet to the walkers: busy walkers, L2 touches of the next tiles),
+    C2 tiles (none), long chains (walkers suspended at several windows and
+    carried into the next tiles), edge cases (MPLS / SLL-less restarts,
+    leaves, ICMP pending) and IMIX at odd offsets."""
+    import random
+    rnd = random.Random(seed)
+    c4 = _packets_of(*T.make_batch(T.SYN_IPV6X, 64 * 42))
+    c2 = _packets_of(*T.make_batch(T.SYN_UDP64, 64 * 18))
+    c3 = _packets_of(*T.make_batch(T.SYN_IMIX, 64 * 6))
+    lc = _long_chains(64 * 12, seed=seed)
+    ed = edge_cases.cases()
+    src = {"c4": c4, "c2": c2, "c3": c3, "lc": lc}
+    order = ["c4", "c4", "c4", "c2", "lc", "c4", "c3", "c4", "c4", "lc", "c2", "c2", "c4", "ed"] * 6
+    pkts = []
+    for k in order:
+        if k == "ed":
+            pkts += [ed[rnd.randrange(len(ed))] for _ in range(64)]
+        else:
+            pkts += [src[k].pop() for _ in range(64)]
+    return pkts
+
+
+@pytest.mark.parametrize("grid", [1, 3, 0])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_walker_pool_mixed_tiles(grid, mode):
+    """The general walk's walker pool under few blocks (grid 1: four waves
+    walk every tile, so walkers carry across many fast walks, refill mid
+    session and drain at the end) over tiles that alternate between
+    walker-heavy, walker-free and deep-chain kinds: records, ext chains and
+    counters equal the oracle's, for both record forms."""
+    import torch
+    frames, desc = T.batch_from_packets(_mixed_tiles(), align=2)
+    orec, oext, ocnt, _ = T.oracle_records(frames, desc, mode=mode)
+    f = torch.from_numpy(frames).cuda()
+    d = torch.from_numpy(desc.view(np.int64)).cuda()
+    rec, ext, ext_used, counters = nsd.dissect_device(f, d, mode=mode, grid=grid)
+    torch.cuda.synchronize()
+    drec = rec.cpu().numpy().view(nsd.REC_DTYPE)
+    dext = ext.cpu().numpy().view(np.uint32)[:int(ext_used.item())]
+    assert_same_records(drec, orec, dext, oext)
+    assert np.array_equal(counters.cpu().numpy().view(np.uint64), ocnt)
+    if grid == 0:
+        _check_compact(frames, desc, mode)
