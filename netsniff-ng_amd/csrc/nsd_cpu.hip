@@ -5,7 +5,7 @@
 // device (nsd_kernels.hip); nothing here is a fallback for them.
 //
 // This is the product's own layer step, gen_step() of nsd_walk.h (the code
-// pass 2 of the device kernel runs), instantiated with a host byte source
+// general walk of the device kernel runs), instantiated with a host byte source
 // over the whole frame and a sink that keeps the chain in arrays:
 //   * nsd_walk_packet_cpu: one packet -> the record (+ ext entry) the device
 //     writes for it;

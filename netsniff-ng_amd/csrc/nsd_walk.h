@@ -10,7 +10,7 @@
 //
 // The byte source (Src) and the sink for what a layer records (Sink) are
 // template parameters, so the same layer step runs
-//   * on the device over an LDS-staged header window (pass 2 of
+//   * on the device over an LDS-staged header window (the general walk of
 //     nsd_kernels.hip: wave-level sinks, ballots, LDS counters), and
 //   * on the host over the whole frame (nsd_cpu.hip: the per-packet entry
 //     point dissector_entry_point and the exported proto-ops objects, which
@@ -107,8 +107,6 @@ struct GenSink {
 	                              // side words [0, n) come first)
 	uint32_t *side;               // compact records: side word of packet i (or null)
 
-	// wave-uniform branch condition: some lane needs the body
-	__device__ __forceinline__ bool any(bool c) const { return __ballot(c) != 0; }
 	// a chain reaching layer 6 + NSD_LDS_LAYERS takes its pool entry now (rare)
 	__device__ __forceinline__ void take_deep(bool deep_first, WalkOut &w) const;
 	// count layer k (ops id, start offset) and keep it beyond the record
@@ -198,7 +196,6 @@ struct HostSink {
 	uint16_t *offs;               // [NSD_EXT_MAX_LAYERS]
 	uint64_t *counters;           // NSD_NCOUNTERS, or NULL
 
-	__host__ bool any(bool c) const { return c; }
 	__host__ void take_deep(bool, WalkOut &) const {}
 	__host__ void layer(const WalkOut &, uint32_t k, int id, uint32_t start) const
 	{
@@ -361,14 +358,17 @@ NSD_HD int sll_next(uint32_t hatype, uint32_t proto, int mode, uint32_t e2)
 // (proto_ipv6_mobility_hdr.c:206-245), one byte per type
 #define NSD_MH_SUB 0x0A060612120A0A02ull
 
-// The general walk (pass 2), one layer per call for every lane of the wave:
+// The general walk (the walkers of nsd_kernels.hip), one layer per call for
+// every lane of the wave:
 // dissector_main's loop body (dissector.c:51-58) for the ops `w.id`,
 // computed as straight-line selects over a per-ops rule table rather than a
 // switch, so a wave whose lanes sit at different layers runs one instruction
 // stream (a divergent switch runs every case body present plus its exec-mask
-// bookkeeping, which made the scalar unit the bottleneck).  The rare heavy
-// bodies (IPv4 header checksum, ICMPv4 checksum, MPLS label walk) sit behind
-// wave-uniform branches.  `act`: the lane runs a layer in this call.  Per
+// bookkeeping, which made the scalar unit the bottleneck).  The rules of the
+// less common kinds and the rare heavy bodies (IPv4 header checksum, ICMPv4
+// checksum, MPLS label walk) are branches only the lanes on such a layer take
+// (the wave skips a body none of its lanes needs; as wave-uniform ballot
+// tests they cost C4 2 % more).  `act`: the lane runs a layer in this call.  Per
 // layer: record the ops (chain word / offsets, or the ext pool entry once
 // the chain needs the ext form), count it, advance the pkt_buff cursor
 // exactly as the reference parser does, look up the next ops.
@@ -410,15 +410,15 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	// the next-ops key's bytes: the layer's first byte for the extension
 	// headers (kpos 0), a second read only when a lane's key sits further on
 	uint32_t KD = B0;
-	if (g.any(act & (kpos != 0)))
+	if (act & (kpos != 0))
 		KD = s.dword_at(start + kpos);
 	const uint32_t b0 = B0 & 0xFF, b1 = (B0 >> 8) & 0xFF, b2 = (B0 >> 16) & 0xFF;
 	// eth_lay2 (a 16-bit ethertype; the perfect hash) / eth_lay3 (dissector_eth.c:30-62)
 	int nx = s.lay3(KD & 0xFF);
-	if (g.any(act & kw16)) {
+	if (act & kw16) {
 		const uint32_t key16 = __builtin_bswap16((uint16_t)KD);
 		const uint32_t e2 = s.l2h(NSD_L2H(key16));
-		nx = kw16 ? ((e2 & 0xFFFF) == key16 ? (int)(e2 >> 16) : 0) : nx;
+		nx = (e2 & 0xFFFF) == key16 ? (int)(e2 >> 16) : 0;
 	}
 	const uint32_t T8 = (b1 + 1u) * 8u;             // (hdr_ext_len + 1) * 8
 	const bool pulled = len >= minl;
@@ -426,39 +426,39 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	// HBH / DestOpts: opt_len = T8 - 2 <= pkt_len after the 2-byte pull;
 	// Routing: data_len = T8 - 4 <= pkt_len after the 4-byte pull.  These,
 	// the fixed pulls and the leaves are the common case; the other kinds'
-	// rules run behind wave-uniform branches (only when a lane of the wave
-	// is on such a layer: VALU issue bounds the general walk)
+	// rules run only when a lane of the wave is on such a layer (instruction
+	// issue bounds the general walk)
 	const bool t8ok = T8 <= len;
 	uint32_t adv = kind == K_T8 ? (t8ok ? T8 : minl) : fadv;
 	bool cont = (kind == K_CONT) | ((kind == K_T8) & t8ok);
 	bool host = kind == K_HOST;
 	const bool isv4 = act & (kind == K_IPV4);
 	uint32_t ihl = 0;
-	if (g.any(isv4)) {
+	if (isv4) {
 		// IPv4: options pulled if present, else data stays (proto_ipv4.c:136)
 		ihl = b0 & 0xF;
 		const uint32_t opts = (ihl > 5 ? ihl : 5) * 4u - 20u;
 		const uint32_t v4adv = 20 + (opts <= len - 20 ? opts : 0);
-		adv = isv4 ? v4adv : adv;
-		cont = cont | isv4;
+		adv = v4adv;
+		cont = true;
 		if (MODE == PRINT_NORM) {
 			// tail trim to tot_len - ihl*4, evaluated in size_t (:174-175)
 			const uint32_t k2 = __builtin_bswap16((uint16_t)(B0 >> 16));   // tot_len
 			const int64_t x = (int64_t)k2 - (int64_t)ihl * 4;
-			const bool trim = isv4 & pulled & (x >= 0) & ((uint64_t)x < len - v4adv);
+			const bool trim = pulled & (x >= 0) & ((uint64_t)x < len - v4adv);
 			w.tail = trim ? start + v4adv + (uint32_t)x : w.tail;
 		}
 	}
 	const bool isah = act & (kind == K_AH);
-	if (g.any(isah)) {
+	if (isah) {
 		// AH: hdr_len = plen*4 + 8, checked after the 12-byte pull, ICV pulled
 		const uint32_t hl = b1 * 4u + 8u;
 		const bool ahok = hl <= len - 12;
-		adv = isah ? 12 + ((ahok & (hl > 12)) ? hl - 12 : 0) : adv;
-		cont = cont | (isah & ahok);
+		adv = 12 + ((ahok & (hl > 12)) ? hl - 12 : 0);
+		cont = ahok;
 	}
 	const bool ismob = act & (kind == K_MOB);
-	if (g.any(ismob)) {
+	if (ismob) {
 		// Mobility: msg_len check, then (PRINT_NORM) get_mh_type's subtype
 		// pull and the second check
 		const int32_t mdl0 = (int32_t)T8 - 6;
@@ -472,17 +472,17 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 		const bool mobok = MODE == PRINT_NORM ? mok1 & mok2 : mok1;
 		const uint32_t mobadv =
 			!mok1 ? 6u : MODE != PRINT_NORM ? T8 : mok2 ? 6 + sp + (uint32_t)mdl : 6 + sp;
-		adv = ismob ? mobadv : adv;
-		cont = cont | (ismob & mobok);
+		adv = mobadv;
+		cont = mobok;
 	}
 	const bool isi6 = act & (kind == K_ICMP6);
-	if (g.any(isi6)) {
+	if (isi6) {
 		// ICMPv6 (PRINT_NORM): types 130-154 have variable-length bodies
 		// (leaf walk); types 1-4 / 128 / 129 pull a 4-byte body
 		const bool i6host = MODE == PRINT_NORM && b0 - 130u <= 24u;
 		const bool i6body = MODE == PRINT_NORM && ((b0 - 1u <= 3u) | ((b0 & 0xFE) == 128)) & (len >= 8);
-		adv = isi6 ? (i6host ? 0u : i6body ? 8u : 4u) : adv;
-		host = host | (isi6 & i6host);
+		adv = i6host ? 0u : i6body ? 8u : 4u;
+		host = i6host;
 	}
 	host = host & pulled;
 	const bool upd = act & (kind != K_MPLS);
@@ -493,31 +493,28 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	// (nsd_leaf.h), so the exit op's dump starts from the record; the
 	// sink decides when (the device walks it after the chain, emit_general)
 	g.template leaf<MODE>(s, upd & host, w, id, start);
-	// ---- the rare heavy bodies, behind wave-uniform branches
+	// ---- the rare heavy bodies
 	const bool v4 = upd && kind == K_IPV4 && pulled;
-	if (MODE == PRINT_NORM && g.any(v4)) {
+	if (MODE == PRINT_NORM && v4) {
 		// checksum over ihl*4 bytes, past the frame too (bytes >= caplen are 0)
-		if (v4)
-			w.ip_csum = calc_csum(s, start, ihl * 2u);
+		w.ip_csum = calc_csum(s, start, ihl * 2u);
 	}
 	const bool i4 = upd && id == NSD_OPS_ICMPV4 && pulled;
-	if (MODE == PRINT_NORM && g.any(i4)) {
+	if (MODE == PRINT_NORM && i4) {
 		// calc_csum(icmp, pkt_len + 8): the whole (post-trim) message, odd
 		// trailing byte dropped (csum.h:24-27); past the window: pending
-		if (i4) {
-			if (s.in_window(start, len & ~1u)) {
-				if (calc_csum(s, start, len >> 1))
-					w.flags |= NSD_F_ICMP_BAD;
-			} else {
-				w.icmp_pend = true;
-				w.icmp_off = start;
-				w.icmp_len = len;
-			}
+		if (s.in_window(start, len & ~1u)) {
+			if (calc_csum(s, start, len >> 1))
+				w.flags |= NSD_F_ICMP_BAD;
+		} else {
+			w.icmp_pend = true;
+			w.icmp_off = start;
+			w.icmp_len = len;
 		}
 	}
 	const bool mp = act && kind == K_MPLS;
-	if (g.any(mp)) {                              // proto_mpls_unicast.c:49-77
-		if (mp) {
+	if (mp) {                                     // proto_mpls_unicast.c:49-77
+		{
 			uint32_t d = start, l = len;
 			bool ok = true;
 			for (;;) {
@@ -543,11 +540,11 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 // as gen_step() for every packet it finishes (the c_step table cites the
 // reference per ops); anything else (MPLS, deeper tag stacks, extension
 // headers, IPv6-in-IPv4, the looping leaves LLDP / IGMP / ICMPv6 130-154,
-// bytes past the staged window) goes to pass 2.  No loop, no per-layer
+// bytes past the staged window) goes to the general walk.  No loop, no per-layer
 // dispatch switch.
-// Returns FW_DONE, FW_RESTART (pass 2 walks the packet from its start) or
+// Returns FW_DONE, FW_RESTART (the general walk takes the packet from its start) or
 // FW_RESUME (the chain reached an extension header / AH / IPv6-in-IPv4 ops
-// at w.data with layers 0..w.n-1 recorded: pass 2 resumes there with w.id).
+// at w.data with layers 0..w.n-1 recorded: the general walk resumes there with w.id).
 enum : uint32_t { FW_DONE = 0, FW_RESTART = 1, FW_RESUME = 2 };
 template <int MODE, class Src>
 __device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, WalkOut &w)
@@ -562,7 +559,7 @@ __device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, Wal
 		n++;
 	};
 	if (w.id != NSD_OPS_ETHERNET)
-		return FW_RESTART;   // other link types: pass 2
+		return FW_RESTART;   // other link types: the general walk
 	rec(NSD_OPS_ETHERNET, 0);
 	if (caplen < 14) {
 		w.n = n;
@@ -690,7 +687,7 @@ __device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, Wal
 	default:
 	resume:
 		// IGMP (its v3 lists run past the window), the ICMPv6 bodies above,
-		// extension headers, AH, IPv6-in-IPv4: pass 2 resumes at d2
+		// extension headers, AH, IPv6-in-IPv4: the general walk resumes at d2
 		if (s.missed())
 			return FW_RESTART;
 		w.n = n;
