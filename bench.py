@@ -122,9 +122,10 @@ class Batch:
         self.ws = torch.empty(nsd.lib().nsd_workspace_bytes(self.n), dtype=torch.uint8, device=dev)
         self.wsum = wsum_for(key, n, lo, shards)
 
-    def step(self, mode, grid=0, ev=None):
-        self.ext_used.zero_()
-        self.counters.zero_()
+    def step(self, mode, grid=0, ev=None, zero=True):
+        if zero:
+            self.ext_used.zero_()
+            self.counters.zero_()
         if ev is not None:
             ev[0].record()
         if self.compact:
@@ -163,14 +164,35 @@ class Batch:
 
 
 def time_steps(b, mode, steps, warmup, grid=0):
-    """Kernel time per launch (HIP events on the launch stream = torch's current one)."""
+    """Kernel time per launch: HIP events on the launch stream (torch's
+    current one) around `steps` back-to-back launches over the resident
+    batch (a capture loop's steady state).  The per-protocol counters
+    accumulate across the launches and must sum to steps x packets.  A
+    workload whose launches take ext-pool words is timed launch by launch
+    instead (each launch needs its pool reset, as the caller does between
+    batches), with one event pair per launch."""
     for _ in range(warmup):
         b.step(mode, grid)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    for k in range(steps):
-        b.step(mode, grid, evs[k])
     torch.cuda.synchronize()
-    return float(np.mean([a.elapsed_time(c) for a, c in evs]))
+    if int(b.ext_used.item()) != 0:
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for k in range(steps):
+            b.step(mode, grid, evs[k])
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(c) for a, c in evs]))
+    b.counters.zero_()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(steps):
+        b.step(mode, grid, zero=False)
+    ev[1].record()
+    torch.cuda.synchronize()
+    cnt = b.counters.cpu().numpy().view(np.uint64)
+    assert int(cnt[nsd.CNT_PKTS]) == steps * b.n and int(b.ext_used.item()) == 0, "counter check failed"
+    b.counters.zero_()
+    b.step(mode, grid)   # leaves one launch's counters for the caller's checks
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / steps
 
 
 # ---- in-run PMC traffic ----------------------------------------------------------
@@ -486,22 +508,36 @@ def main():
         if dist is not None:
             dist.all_reduce(b.counters)
     torch.cuda.synchronize()
+    # one GPU: the K launches back to back, counters accumulating across them
+    # (checked below), one event pair around them (time_steps); more GPUs:
+    # each step's counters summed over the ranks (RCCL), events per launch
+    accumulate = dist is None and int(b.ext_used.item()) == 0
+    if accumulate:
+        b.counters.zero_()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+           for _ in range(1 if accumulate else args.steps)]
     t0 = time.perf_counter()
+    if accumulate:
+        evs[0][0].record()
     for k in range(args.steps):
-        b.step(args.mode, args.grid, evs[k])
+        if accumulate:
+            b.step(args.mode, args.grid, zero=False)
+        else:
+            b.step(args.mode, args.grid, evs[k])
         if dist is not None:
             dist.all_reduce(b.counters)   # RCCL over xGMI: per-protocol counters
+    if accumulate:
+        evs[0][1].record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(c) for a, c in evs]))
+    kern_ms = (evs[0][0].elapsed_time(evs[0][1]) / args.steps if accumulate
+               else float(np.mean([a.elapsed_time(c) for a, c in evs])))
     if dist is not None:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -509,7 +545,8 @@ def main():
 
     cnt = b.counters.cpu().numpy().view(np.uint64)
     total_pkts = b.n * world
-    assert int(cnt[nsd.CNT_PKTS]) == total_pkts, "counter check failed"
+    assert int(cnt[nsd.CNT_PKTS]) == total_pkts * (args.steps if accumulate else 1), "counter check failed"
+    assert not accumulate or int(b.ext_used.item()) == 0, "ext pool used while accumulating"
     ms_per_step = elapsed / args.steps * 1e3
     mpps = total_pkts * args.steps / elapsed / 1e6
 
