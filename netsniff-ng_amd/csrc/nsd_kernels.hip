@@ -473,6 +473,7 @@ constexpr int WINWORDS = 64 * row_of(WIN1) > 16 * WIN2 ? 64 * row_of(WIN1) : 16 
 struct Shared {
 	alignas(16) uint32_t win[WAVES][WINWORDS];              // staged windows (fast walk, then continuations)
 	unsigned long long cnt[NSD_NCOUNTERS];      // block counters
+	uint32_t ops[32];                           // block per-ops layer counts (32-bit LDS atomics)
 	uint8_t lay3[256];                          // eth_lay3
 	uint32_t step[64];                          // c_step, c_lay2h (general walk)
 	uint32_t wc[WAVES][2];                      // per-wave ext pool chunk {next word, words left}
@@ -492,7 +493,7 @@ __device__ __forceinline__ void sll_head(Shared &sh, WalkOut &w, const uint32_t 
 	const uint32_t proto = __builtin_bswap16((uint16_t)(w0 >> 16));
 	w.chain = NSD_OPS_SLL;
 	w.n = 1;
-	atomicAdd(&sh.cnt[NSD_CNT_OPS + NSD_OPS_SLL], 1ull);
+	atomicAdd(&sh.ops[NSD_OPS_SLL], 1u);
 	w.id = sll_next(hatype, proto, MODE, sh.step[32 + NSD_L2H(proto)]);
 }
 
@@ -740,7 +741,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	// compact records: pool words [0, n) are the packets' side words (when the
 	// pool has them), entries come after
 	const bool side = CR && ext_words >= n;
-	const GenSink<CR> g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.cnt, &sh.lay[wv][0],
+	const GenSink<CR> g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.ops, &sh.lay[wv][0],
 			 side ? n : 0u, side ? ext : nullptr };
 	FlagCnt fc;
 	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
@@ -834,7 +835,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 						// count their own layers (the LDS serialises them)
 						if (key != 0xFFFFFFFFu)
 							for (uint32_t k = 0; k < w.n; k++)
-								atomicAdd(&s_cnt[NSD_CNT_OPS + ((key >> (5 * k)) & 31)], 1ull);
+								atomicAdd(&sh.ops[(key >> (5 * k)) & 31], 1u);
 						break;
 					}
 					const int leader = __ffsll((unsigned long long)pm) - 1;
@@ -843,8 +844,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 					if (lane == leader) {
 						const uint32_t cnt = (uint32_t)__popcll(m);
 						for (uint32_t k = 0, nl = w.n; k < nl; k++)
-							atomicAdd(&s_cnt[NSD_CNT_OPS + ((lk >> (5 * k)) & 31)],
-								  (unsigned long long)cnt);
+							atomicAdd(&sh.ops[(lk >> (5 * k)) & 31], cnt);
 					}
 					if (key == lk)
 						key = 0xFFFFFFFFu;
@@ -865,7 +865,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 						sll_head<MODE>(sh, w, sll, i);
 				} else {
 					for (uint32_t k = 0; k < w.n; k++)
-						atomicAdd(&s_cnt[NSD_CNT_OPS + ((w.chain >> (5 * k)) & 31)], 1ull);
+						atomicAdd(&sh.ops[(w.chain >> (5 * k)) & 31], 1u);
 				}
 			}
 		}
@@ -1013,6 +1013,8 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	__shared__ Shared sh;
 	if (threadIdx.x < 64)
 		sh.step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h.e[threadIdx.x - 32];
+	if (threadIdx.x < 32)
+		sh.ops[threadIdx.x] = 0;
 	if (threadIdx.x < 2 * WAVES)
 		sh.wc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
 	block_init(sh.cnt, sh.lay3);   // (its barrier orders the stores above too)
@@ -1030,6 +1032,8 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 		icmp_pass<NSD_CSUM_U, CR>(sh, frames, desc, rec, pend, region);
 	}
 	block_flush(sh.cnt, counters);
+	if (threadIdx.x < 32 && sh.ops[threadIdx.x])
+		atomicAdd(&counters[NSD_CNT_OPS + threadIdx.x], (unsigned long long)sh.ops[threadIdx.x]);
 }
 
 

@@ -101,7 +101,7 @@ struct GenSink {
 	uint32_t *used;               // pool words handed out (global)
 	uint32_t chunk;               // words per chunk request
 	uint32_t *wc;                 // LDS: this wave's chunk {next word, words left}
-	unsigned long long *s_cnt;    // LDS: block counters
+	uint32_t *s_ops;              // LDS: block per-ops layer counts
 	uint32_t *lay;                // LDS: this wave's layer lists, [j * 64 + lane]
 	uint32_t sbase;               // first pool word handed out (compact records: the
 	                              // side words [0, n) come first)
@@ -166,7 +166,7 @@ template <bool CR>
 __device__ __forceinline__ void GenSink<CR>::layer(const WalkOut &w, uint32_t k, int id, uint32_t start) const
 {
 	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
-	atomicAdd(&s_cnt[NSD_CNT_OPS + id], 1ull);   // the oracle counts the first 64 layers
+	atomicAdd(&s_ops[id], 1u);   // the oracle counts the first 64 layers
 	const uint32_t lv = CR ? (uint32_t)id : (uint32_t)id | start << 16;
 	if (!CR && k >= NSD_REC_MAX_LAYERS && k < DEEP)
 		lay[(k - NSD_REC_MAX_LAYERS) * 64 + __lane_id()] = lv;
@@ -378,6 +378,9 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	const int id = act ? w.id : 0;
 	const uint32_t start = w.data;
 	const uint32_t k = w.n;
+	// the ops' rule word (read before the sink's stores, so the device walk's
+	// near_end() read of the same word serves it)
+	const uint32_t info = act ? s.step(w.id) : 0u;
 	// ---- record the layer: the first 6 in the record; more than 6, or a
 	// layer past byte 510, forces the ext form
 	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
@@ -402,7 +405,6 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	// computed for every lane and selected by the rule kind (boolean terms
 	// combined with & and | so the compiler keeps them as selects).
 	const uint32_t len = w.tail - start;   // pkt_len (pkt_buff.h:36-41)
-	const uint32_t info = s.step(id);
 	const uint32_t minl = info & 0xFF, fadv = (info >> 8) & 0xFF, kind = (info >> 16) & 0xF,
 		       kpos = (info >> 20) & 0xF;
 	const bool kw16 = (info >> 24) & 1;
