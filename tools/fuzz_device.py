@@ -1,5 +1,7 @@
 """Device vs oracle on seeded mutation-fuzz batches (tests/fuzz_cases.py),
-several seeds, modes and alignments; prints mismatch counts.  GPU box tool:
+several seeds, modes and alignments, both record forms (16-byte records
+through the host batch entry, compact records through the device-resident
+entry); prints mismatch counts.  GPU box tool:
   python tools/fuzz_device.py [n] [seeds]"""
 import os
 import sys
@@ -12,7 +14,7 @@ import numpy as np  # noqa: E402
 import fuzz_cases  # noqa: E402
 import nsd  # noqa: E402
 import nsd_testlib as T  # noqa: E402
-from test_device_parity import assert_same_records  # noqa: E402
+from test_device_parity import _check_compact, assert_same_records  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 200000
 seeds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
@@ -25,7 +27,9 @@ for seed in range(seeds):
         try:
             assert_same_records(rec, orec, ext, oext)
             assert np.array_equal(cnt, ocnt), "counters differ"
-            print(f"seed {1000 + seed} mode {mode} align {align}: {n} records identical", flush=True)
+            _check_compact(frames, desc, mode)
+            print(f"seed {1000 + seed} mode {mode} align {align}: {n} records identical (16-B and compact)",
+                  flush=True)
         except AssertionError as e:
             fails += 1
             print(f"seed {1000 + seed} mode {mode} align {align}: MISMATCH {e}", flush=True)
