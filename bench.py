@@ -163,6 +163,31 @@ class Batch:
             setattr(self, a, None)
 
 
+WARM_SECONDS = 0.25
+
+
+def warm(b, mode, warmup, grid=0, seconds=WARM_SECONDS, reduce=None):
+    """The untimed warmup: launches for `seconds`, then `warmup` launches,
+    so the timed region starts at the GPU's steady clocks (3 launches of
+    0.25 ms leave it ramping: C2 measured 0.262 ms after them, 0.249 after
+    0.25 s of launches, on one box).  `reduce` (the multi-GPU counter
+    all-reduce) follows each of the `warmup` launches only: the timed part
+    of the warmup runs a different number of launches on each rank, so it
+    holds no collective."""
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        b.step(mode, grid)
+        k += 1
+        if k % 16 == 0:
+            torch.cuda.synchronize()
+    for _ in range(warmup):
+        b.step(mode, grid)
+        if reduce is not None:
+            reduce()
+    torch.cuda.synchronize()
+
+
 def time_steps(b, mode, steps, warmup, grid=0):
     """Kernel time per launch: HIP events on the launch stream (torch's
     current one) around `steps` back-to-back launches over the resident
@@ -171,9 +196,7 @@ def time_steps(b, mode, steps, warmup, grid=0):
     workload whose launches take ext-pool words is timed launch by launch
     instead (each launch needs its pool reset, as the caller does between
     batches), with one event pair per launch."""
-    for _ in range(warmup):
-        b.step(mode, grid)
-    torch.cuda.synchronize()
+    warm(b, mode, warmup, grid)
     if int(b.ext_used.item()) != 0:
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         for k in range(steps):
@@ -503,11 +526,8 @@ def main():
     compact = args.records == "compact"
     b = Batch(args.config, n, lo, args.shards, dev, compact=compact)
 
-    for _ in range(args.warmup):
-        b.step(args.mode, args.grid)
-        if dist is not None:
-            dist.all_reduce(b.counters)
-    torch.cuda.synchronize()
+    warm(b, args.mode, args.warmup, args.grid,
+         reduce=None if dist is None else (lambda: dist.all_reduce(b.counters)))
     # one GPU: the K launches back to back, counters accumulating across them
     # (checked below), one event pair around them (time_steps); more GPUs:
     # each step's counters summed over the ranks (RCCL), events per launch

@@ -56,29 +56,46 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "round")):
                                          "average_us": float(row["AverageNs"]) / 1e3}
         bench = last_json(os.path.join(src, "stats.log"))
         check = {"rocprof_stats": rows}
-        # per workload: the bench launches dissect_all in this order, warmup +
-        # steps each: headline (compact), other record form, then each leg
+        # per workload: the bench launches dissect_all per workload in this
+        # order (headline compact, the other record form, then each leg),
+        # each a run of warmup launches (a time-based part: any count) + the
+        # timed steps (+ one launch after them for the legs' counter checks,
+        # bench.time_steps); the workloads are apart by seconds of batch
+        # generation, so a gap of > 50 ms splits them
         tr = os.path.join(src, "stats", "run_kernel_trace.csv")
         if os.path.exists(tr) and bench:
             b = json.loads(bench)
-            per = b["steps"] + b["warmup"]
+            steps = b["steps"]
             d = {}
             with open(tr) as f:
                 for row in csv.DictReader(f):
                     if "dissect_all" in row["Kernel_Name"]:
                         d.setdefault(row["Kernel_Name"].split("(")[0], []).append(
-                            (int(row["Dispatch_Id"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3))
+                            (int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+
+            def runs(ds):
+                ds = sorted(ds)
+                out, cur = [], []
+                for s0, e0 in ds:
+                    if cur and s0 - cur[-1][1] > 50_000_000:
+                        out.append(cur)
+                        cur = []
+                    cur.append((s0, e0))
+                if cur:
+                    out.append(cur)
+                return out
+
+            def avg_us(seg):
+                return round(sum(e0 - s0 for s0, e0 in seg) / len(seg) / 1e3, 1) if seg else None
+
             names = ["headline"] + list((b.get("legs") or {}).keys())
-            compact = sorted(d.get("void nsd::dissect_all<0, true>", []))
-            full = sorted(d.get("void nsd::dissect_all<0, false>", []))
             split = {}
-            for k, name in enumerate(names):
-                seg = compact[k * per:(k + 1) * per][b["warmup"]:]
-                if seg:
-                    split[name] = round(sum(x for _, x in seg) / len(seg), 1)
+            for k, run in enumerate(runs(d.get("void nsd::dissect_all<0, true>", []))):
+                if k < len(names):
+                    split[names[k]] = avg_us(run[-steps:] if k == 0 else run[-steps - 1:-1])
+            full = runs(d.get("void nsd::dissect_all<0, false>", []))
             if full:
-                seg = full[b["warmup"]:]
-                split["other_records"] = round(sum(x for _, x in seg) / len(seg), 1)
+                split["other_records"] = avg_us(full[0][-steps - 1:-1])
             check["rocprof_trace_avg_us"] = split
         if bench:
             b = json.loads(bench)
