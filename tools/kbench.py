@@ -42,8 +42,9 @@ def main():
             print(f"{key:6s} rec{b.rec_b:<2d} kernel_ms={ms:.4f} frac={r['frac'] if r else None} "
                   f"read_frac={r['read_frac'] if r else None} pkts_counted={int(cnt[32])}", flush=True)
             if os.environ.get("KB_PHASES"):
-                # counters 48..55 of an instrumented variant (tools/variants/phases.patch):
-                # per-wave clock sums of the last launch
+                # counters 48..55 of an instrumented variant (tools/variants/phases.patch),
+                # summed over waves, last launch: fast-walk part, walker engine, window
+                # staging, layer steps, emit (cycles), sessions, step iterations, take (cycles)
                 print(f"{key:6s} phases {[int(x) for x in cnt[48:56]]}", flush=True)
             b.free()
             torch.cuda.empty_cache()
