@@ -528,10 +528,17 @@ def main():
 
     warm(b, args.mode, args.warmup, args.grid,
          reduce=None if dist is None else (lambda: dist.all_reduce(b.counters)))
-    # one GPU: the K launches back to back, counters accumulating across them
-    # (checked below), one event pair around them (time_steps); more GPUs:
-    # each step's counters summed over the ranks (RCCL), events per launch
-    accumulate = dist is None and int(b.ext_used.item()) == 0
+    # the K launches back to back, counters accumulating across them (checked
+    # below), one event pair around them; with more GPUs the counter vectors
+    # are summed over the ranks by one RCCL all-reduce after the K launches,
+    # inside the timed region.  A workload whose launches take ext-pool words
+    # (none of the bench's) is timed launch by launch with its pool and
+    # counters reset before each, as a caller does between batches.
+    accumulate = int(b.ext_used.item()) == 0
+    if dist is not None:
+        flag = torch.tensor([1 if accumulate else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        accumulate = bool(flag.item())
     if accumulate:
         b.counters.zero_()
     if dist is not None:
@@ -542,15 +549,16 @@ def main():
     t0 = time.perf_counter()
     if accumulate:
         evs[0][0].record()
-    for k in range(args.steps):
-        if accumulate:
+        for _ in range(args.steps):
             b.step(args.mode, args.grid, zero=False)
-        else:
-            b.step(args.mode, args.grid, evs[k])
+        evs[0][1].record()
         if dist is not None:
             dist.all_reduce(b.counters)   # RCCL over xGMI: per-protocol counters
-    if accumulate:
-        evs[0][1].record()
+    else:
+        for k in range(args.steps):
+            b.step(args.mode, args.grid, evs[k])
+            if dist is not None:
+                dist.all_reduce(b.counters)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
