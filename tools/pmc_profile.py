@@ -1,0 +1,58 @@
+"""Per-config PMC summary of the dissect kernel from tools/gpu_pmc.sh runs
+(gpurun_out/pmc/<cfg>_<pass>/): per-packet HBM bytes (FETCH_SIZE doubled,
+the gfx950 wide-read correction, checked against the 128-B request count),
+WRITE_SIZE, instruction counts per 64-packet tile, wave-cycle split.
+  python tools/pmc_profile.py out.json udp64 imix ipv6x"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PACKETS = 1 << 24
+
+
+def counters(cfg):
+    per = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(ROOT, "gpurun_out", "pmc", f"{cfg}_*", "**", "*counter_collection.csv"),
+                       recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "dissect_all<0, true>" in r["Kernel_Name"]:
+                per[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}
+
+
+def summary(cfg):
+    c = counters(cfg)
+    tiles = PACKETS / 64
+    out = {"packets": PACKETS}
+    if "FETCH_SIZE" in c:
+        out["fetch_bytes_per_pkt"] = round(2 * c["FETCH_SIZE"] * 1024 / PACKETS, 1)
+    if "TCC_EA0_RDREQ_sum" in c:
+        out["read_requests_per_pkt"] = round(c["TCC_EA0_RDREQ_sum"] / PACKETS, 3)
+        out["read_request_bytes_per_pkt"] = round(128 * c.get("TCC_EA0_RDREQ_128B_sum", 0) / PACKETS
+                                                  + 64 * c.get("TCC_EA0_RDREQ_64B_sum", 0) / PACKETS
+                                                  + 32 * c.get("TCC_EA0_RDREQ_32B_sum", 0) / PACKETS, 1)
+    if "WRITE_SIZE" in c:
+        out["write_bytes_per_pkt"] = round(c["WRITE_SIZE"] * 1024 / PACKETS, 1)
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_INSTS_VMEM_RD",
+              "SQ_INSTS_VMEM_WR"):
+        if k in c:
+            out[k.lower().replace("sq_insts_", "") + "_per_tile"] = round(c[k] / tiles, 1)
+    if "SQ_WAVE_CYCLES" in c:
+        wc = c["SQ_WAVE_CYCLES"]
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if k in c:
+                out[k.lower() + "_frac"] = round(c[k] / wc, 3)
+    if "SQ_LDS_BANK_CONFLICT" in c:
+        out["lds_bank_conflict_cycles_per_tile"] = round(c["SQ_LDS_BANK_CONFLICT"] / tiles, 1)
+    return out
+
+
+if __name__ == "__main__":
+    res = {cfg: summary(cfg) for cfg in sys.argv[2:]}
+    with open(sys.argv[1], "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
