@@ -47,6 +47,7 @@ sys.path.insert(0, os.path.join(ROOT, "netsniff-ng_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import nsd  # noqa: E402
+import nsd_dist  # noqa: E402
 import nsd_testlib as T  # noqa: E402  (input generators; oracle only in cpu_baseline)
 
 CONFIGS = {
@@ -162,6 +163,70 @@ class Batch:
         for a in ("frames", "desc", "rec", "ext", "ext_used", "counters", "ws"):
             setattr(self, a, None)
 
+    @staticmethod
+    def event():
+        return torch.cuda.Event(enable_timing=True)
+
+    @staticmethod
+    def sync():
+        torch.cuda.synchronize()
+
+
+class HostEvent:
+    """torch.cuda.Event's timing interface on the host clock."""
+
+    def __init__(self):
+        self.t = None
+
+    def record(self):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+class HostBatch:
+    """The rank body's batch for the CPU tests (tests/test_multi.py, gloo):
+    the same packets a GPU rank would hold, walked by the product's host
+    walk (nsd.walk_cpu -> nsd_walk_packet_cpu, the layer step the per-packet
+    dissector_entry_point runs) instead of the kernel, so measure_rank()'s
+    sharding, timing and counter reduce run unchanged without a GPU.  Never
+    used by a bench run."""
+
+    def __init__(self, key, n, lo, shards, compact=True):
+        self.key, self.n_shard, self.shards, self.compact = key, n, shards, compact
+        self.rec_b = CREC_B if compact else REC_B
+        self.n = n * shards
+        self.frames, self.desc = T.make_batch(CONFIGS[key]["cfg"], self.n, lo=lo)
+        self.frame_bytes = int(T.desc_caplen(self.desc).sum())
+        self.counters = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64)
+        self.ext_used = torch.zeros(1, dtype=torch.int32)
+        self.wsum = None
+
+    def step(self, mode, grid=0, ev=None, zero=True):
+        if zero:
+            self.counters.zero_()
+        if ev is not None:
+            ev[0].record()
+        _, _, cnt = nsd.walk_cpu(self.frames, self.desc, mode=mode)
+        self.counters += torch.from_numpy(cnt.view(np.int64))
+        if ev is not None:
+            ev[1].record()
+
+    def roofline(self, *a, **k):
+        return None
+
+    def free(self):
+        self.frames = self.desc = None
+
+    @staticmethod
+    def event():
+        return HostEvent()
+
+    @staticmethod
+    def sync():
+        pass
+
 
 WARM_SECONDS = 0.25
 
@@ -180,12 +245,12 @@ def warm(b, mode, warmup, grid=0, seconds=WARM_SECONDS, reduce=None):
         b.step(mode, grid)
         k += 1
         if k % 16 == 0:
-            torch.cuda.synchronize()
+            b.sync()
     for _ in range(warmup):
         b.step(mode, grid)
         if reduce is not None:
             reduce()
-    torch.cuda.synchronize()
+    b.sync()
 
 
 def time_steps(b, mode, steps, warmup, grid=0):
@@ -471,7 +536,64 @@ def copy_rate(dev):
     return gbs
 
 
-def main():
+def measure_rank(args, rank, world, dev, engine="device"):
+    """One rank's measurement (the whole job at N = 1): its weak shard of
+    args.packets x args.shards packets [rank * per_rank, ...) resident, the
+    untimed warmup, then exactly args.steps launches between a barrier +
+    sync on both sides, the per-protocol counters summed over the ranks by
+    one all-reduce inside the timed region (RCCL over xGMI; gloo in the CPU
+    test) and the times maxed over the ranks (nsd_dist).  Counters must come
+    to world x packets x steps.  engine "host" (tests/test_multi.py only)
+    walks the shard with the product's host walk instead of the kernel.
+    Returns (batch, info dict)."""
+    per_rank = args.packets * args.shards
+    lo, _ = nsd_dist.weak_shard(per_rank, rank)
+    compact = args.records == "compact"
+    if engine == "device":
+        b = Batch(args.config, args.packets, lo, args.shards, dev, compact=compact)
+    else:
+        b = HostBatch(args.config, args.packets, lo, args.shards, compact=compact)
+    multi = nsd_dist.initialized()
+    warm(b, args.mode, args.warmup, args.grid,
+         seconds=WARM_SECONDS if engine == "device" else 0.0,
+         reduce=(lambda: nsd_dist.reduce_counters(b.counters)) if multi else None)
+    # the K launches back to back, counters accumulating across them; a
+    # workload whose launches take ext-pool words (none of the bench's) is
+    # timed launch by launch with its pool and counters reset before each,
+    # as a caller does between batches
+    accumulate = nsd_dist.all_ranks_agree(int(b.ext_used.item()) == 0, dev)
+    if accumulate:
+        b.counters.zero_()
+    nsd_dist.barrier()
+    b.sync()
+    evs = [(b.event(), b.event()) for _ in range(1 if accumulate else args.steps)]
+    t0 = time.perf_counter()
+    if accumulate:
+        evs[0][0].record()
+        for _ in range(args.steps):
+            b.step(args.mode, args.grid, zero=False)
+        evs[0][1].record()
+        nsd_dist.reduce_counters(b.counters)
+    else:
+        for k in range(args.steps):
+            b.step(args.mode, args.grid, evs[k])
+            nsd_dist.reduce_counters(b.counters)
+    b.sync()
+    nsd_dist.barrier()
+    b.sync()
+    elapsed = time.perf_counter() - t0
+    kern_ms = (evs[0][0].elapsed_time(evs[0][1]) / args.steps if accumulate
+               else float(np.mean([a.elapsed_time(c) for a, c in evs])))
+    elapsed, kern_ms = nsd_dist.max_over_ranks([elapsed, kern_ms], dev)
+    cnt = b.counters.cpu().numpy().view(np.uint64).copy()
+    total_pkts = b.n * world
+    assert int(cnt[nsd.CNT_PKTS]) == total_pkts * (args.steps if accumulate else 1), "counter check failed"
+    assert not accumulate or int(b.ext_used.item()) == 0, "ext pool used while accumulating"
+    return b, {"elapsed": elapsed, "kern_ms": kern_ms, "counters": cnt, "total_pkts": total_pkts,
+               "accumulate": accumulate, "frame_bytes": b.frame_bytes}
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -484,7 +606,7 @@ def main():
     ap.add_argument("--records", default="compact", choices=["compact", "full"],
                     help="record form of the timed launches: 8-byte nsd_crec or 16-byte nsd_rec")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="CPU baseline duration (4 legs)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline duration (all legs)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end pass")
     ap.add_argument("--no-bpf", action="store_true", help="skip the device BPF filter pass")
     ap.add_argument("--no-replay", action="store_true", help="skip the pcap replay (--in) pass")
@@ -496,14 +618,27 @@ def main():
     ap.add_argument("--e2e-depth", type=int, default=3)
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-configs", default="", help=argparse.SUPPRESS)
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
     if args.pmc_child:
         pmc_child(args)
         return
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = nsd_dist.rank_env()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here, as fresh processes, before this
+        # one touches a GPU (counting devices initialises none)
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr)
+            sys.exit(2)
+        sys.exit(nsd_dist.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} under a launcher of {world} ranks", file=sys.stderr)
+        sys.exit(2)
     solo = rank == 0 and world == 1
     legs = [k for k in LEGS if k != args.config] if solo and not args.no_legs else []
 
@@ -513,68 +648,15 @@ def main():
         traffic = pmc_traffic(args, [args.config] + legs)
 
     if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        nsd_dist.init("nccl", local)
     else:
-        dist = None
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
-
     n = args.packets
-    lo = rank * n * args.shards
     compact = args.records == "compact"
-    b = Batch(args.config, n, lo, args.shards, dev, compact=compact)
 
-    warm(b, args.mode, args.warmup, args.grid,
-         reduce=None if dist is None else (lambda: dist.all_reduce(b.counters)))
-    # the K launches back to back, counters accumulating across them (checked
-    # below), one event pair around them; with more GPUs the counter vectors
-    # are summed over the ranks by one RCCL all-reduce after the K launches,
-    # inside the timed region.  A workload whose launches take ext-pool words
-    # (none of the bench's) is timed launch by launch with its pool and
-    # counters reset before each, as a caller does between batches.
-    accumulate = int(b.ext_used.item()) == 0
-    if dist is not None:
-        flag = torch.tensor([1 if accumulate else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        accumulate = bool(flag.item())
-    if accumulate:
-        b.counters.zero_()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(1 if accumulate else args.steps)]
-    t0 = time.perf_counter()
-    if accumulate:
-        evs[0][0].record()
-        for _ in range(args.steps):
-            b.step(args.mode, args.grid, zero=False)
-        evs[0][1].record()
-        if dist is not None:
-            dist.all_reduce(b.counters)   # RCCL over xGMI: per-protocol counters
-    else:
-        for k in range(args.steps):
-            b.step(args.mode, args.grid, evs[k])
-            if dist is not None:
-                dist.all_reduce(b.counters)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = (evs[0][0].elapsed_time(evs[0][1]) / args.steps if accumulate
-               else float(np.mean([a.elapsed_time(c) for a, c in evs])))
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
-    cnt = b.counters.cpu().numpy().view(np.uint64)
-    total_pkts = b.n * world
-    assert int(cnt[nsd.CNT_PKTS]) == total_pkts * (args.steps if accumulate else 1), "counter check failed"
-    assert not accumulate or int(b.ext_used.item()) == 0, "ext pool used while accumulating"
+    b, m = measure_rank(args, rank, world, dev)
+    elapsed, kern_ms, total_pkts = m["elapsed"], m["kern_ms"], m["total_pkts"]
     ms_per_step = elapsed / args.steps * 1e3
     mpps = total_pkts * args.steps / elapsed / 1e6
 
@@ -589,7 +671,7 @@ def main():
     # the other record form over the same workload (kernel time, roofline)
     other = None
     if solo and not args.no_legs:
-        ob = Batch(args.config, n, lo, args.shards, dev, compact=not compact)
+        ob = Batch(args.config, n, 0, args.shards, dev, compact=not compact)
         oms = time_steps(ob, args.mode, args.steps, args.warmup, 0)
         other = {"records": "full 16 B (nsd_rec)" if compact else "compact 8 B (nsd_crec)",
                  "value": round(ob.n / (oms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
@@ -636,6 +718,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "gbps_frames": round(frame_bytes * world * args.steps / elapsed / 1e9, 1),
             "roofline": roofline,
+            "counters_total": int(m["counters"][nsd.CNT_PKTS]),
             "legs": leg_out or None,
             "other_records": other,
             "cpu_baseline": cpu,
@@ -646,8 +729,9 @@ def main():
         }
         if isinstance(traffic, dict) and "error" in traffic:
             out["pmc_error"] = traffic["error"]
-        print(json.dumps(out))
-    if dist is not None:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

@@ -8,6 +8,8 @@ ONE MI355X: the 8 contiguous 16M-packet shards of the same seeded stream
   shards' counter vectors sum to the whole batch's (the RCCL all-reduce);
 * every record of all 134,217,728 packets is bit-exact against the CPU
   oracle (multi-threaded fields walk over each shard's host copy);
+* the same for the compact 8-byte records bench.py times (shards vs whole,
+  every record vs nsd.compact_of(oracle), counters);
 * the counters equal the oracle's, and the oracle's sum of algorithmic read
   bytes W per shard equals the committed tests/golden/wsum.json entry
   (the bench's roofline denominator for that shard)."""
@@ -79,3 +81,32 @@ def test_c5_shards_on_one_gpu():
             bad = np.nonzero((got[fld] != want[fld]).reshape(SHARD, -1).any(axis=1))[0]
             assert len(bad) == 0, f"shard {r}: {fld} differs at packets {(bad[:10] + r * SHARD).tolist()}"
     assert np.array_equal(cnt_sum, cnt_all), "sum of shard counters != whole batch"
+    del rec_all, rec_sh
+    torch.cuda.empty_cache()
+
+    # the compact form (the one bench.py times): 8 shards vs the whole batch,
+    # every record against the oracle's (IMIX chains are inline: <= 6 layers)
+    crec_all = torch.empty(n * nsd.CREC_BYTES, dtype=torch.uint8, device="cuda")
+    ccnt_all = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device="cuda")
+    used.zero_()
+    nsd.dissect_device_compact(frames, desc, crec=crec_all, ext=ext, ext_used=used, counters=ccnt_all,
+                               workspace=ws)
+    torch.cuda.synchronize()
+    assert np.array_equal(ccnt_all.cpu().numpy().view(np.uint64), ocnt), "compact whole-batch counters vs oracle"
+    crec_sh = torch.empty(SHARD * nsd.CREC_BYTES, dtype=torch.uint8, device="cuda")
+    csum = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
+    for r in range(SHARDS):
+        cnt_r = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device="cuda")
+        used.zero_()
+        nsd.dissect_device_compact(frames, desc[r * SHARD:(r + 1) * SHARD], crec=crec_sh, ext=ext,
+                                   ext_used=used, counters=cnt_r, workspace=ws)
+        torch.cuda.synchronize()
+        whole = crec_all[r * SHARD * nsd.CREC_BYTES:(r + 1) * SHARD * nsd.CREC_BYTES]
+        assert torch.equal(crec_sh, whole), f"shard {r}: compact shard batch != whole batch"
+        csum += cnt_r.cpu().numpy().view(np.uint64)
+        got = whole.cpu().numpy().view(nsd.CREC_DTYPE)
+        want, _ = nsd.compact_of(orecs[r])
+        for fld in ("chain", "ip_csum", "nflags", "nlayers"):
+            bad = np.nonzero(got[fld] != want[fld])[0]
+            assert len(bad) == 0, f"shard {r}: compact {fld} differs at packets {(bad[:10] + r * SHARD).tolist()}"
+    assert np.array_equal(csum, ocnt), "sum of compact shard counters != oracle"

@@ -103,3 +103,111 @@ def test_full_size_properties(cfg):
             ids = (ext[slots[m] + nsd.EXT_HDR_WORDS + k] & 0xFF).astype(np.int64)
             ops += np.bincount(ids, minlength=32).astype(np.uint64)
     assert np.array_equal(cnt[:32], ops)
+
+
+# ---- the compact record form (nsd_crec: the form bench.py times) -------------------
+def _run_compact(torch, f, d):
+    crec, ext, used, cnt = nsd.dissect_device_compact(f, d, mode=T.PRINT_NORM)
+    torch.cuda.synchronize()
+    n = d.numel()
+    return (crec.cpu().numpy().view(nsd.CREC_DTYPE).copy(),
+            ext.cpu().numpy().view(np.uint32)[:n + int(used.item())].copy(),
+            cnt.cpu().numpy().view(np.uint64).copy())
+
+
+def _cids(crec, pool, i):
+    """Ops ids of compact record i (batch index i): inline, inline + the side
+    word (pool word i), or the ext entry at the record's slot."""
+    r = crec[i]
+    nl, chain = int(r["nflags"]) & 7, int(r["chain"])
+    if nl != 7:
+        return tuple((chain >> (5 * k)) & 31 for k in range(nl))
+    if int(r["nlayers"]):
+        side = int(pool[i])
+        return tuple((chain >> (5 * k)) & 31 for k in range(6)) + tuple(
+            (side >> (5 * (k - 6))) & 31 for k in range(6, int(r["nlayers"])))
+    if chain == 0xFFFFFFFF:
+        return ("overflow",)
+    pkt, ids, offs = nsd.ext_entry(pool, chain)
+    assert pkt == i and not any(offs)
+    return ids
+
+
+def _compact_ops(crec, pool):
+    """Per-ops layer counts tallied over every compact chain (vectorised)."""
+    ops = np.zeros(32, dtype=np.uint64)
+    nl = (crec["nflags"] & 7).astype(np.int64)
+    chain = crec["chain"].astype(np.uint64)
+    for k in range(6):
+        m = (nl != 7) & (nl > k) | (nl == 7) & (crec["nlayers"] > 0)
+        ops += np.bincount(((chain[m] >> np.uint64(5 * k)) & np.uint64(31)).astype(np.int64),
+                           minlength=32).astype(np.uint64)
+    sw = np.nonzero((nl == 7) & (crec["nlayers"] > 0))[0]
+    side = pool[sw].astype(np.uint64)
+    for k in range(6, 12):
+        m = crec["nlayers"][sw] > k
+        ops += np.bincount(((side[m] >> np.uint64(5 * (k - 6))) & np.uint64(31)).astype(np.int64),
+                           minlength=32).astype(np.uint64)
+    for i in np.nonzero((nl == 7) & (crec["nlayers"] == 0))[0]:
+        ids = _cids(crec, pool, int(i))
+        assert ids != ("overflow",)
+        ops += np.bincount(np.array(ids[:nsd.EXT_MAX_LAYERS], dtype=np.int64), minlength=32).astype(np.uint64)
+    return ops
+
+
+@pytest.mark.parametrize("cfg", [T.SYN_UDP64, T.SYN_IMIX, T.SYN_IPV6X])
+def test_full_size_compact(cfg):
+    """The headline kernel (dissect_all<PRINT_NORM, compact>) at BASELINE's
+    16,777,216 packets: sampled records (65,536 random + first/last 4,096)
+    equal nsd.compact_of(oracle) field by field with side words and ext
+    entries resolved; determinism; two half batches = the whole; counters =
+    the oracle's tally over the records."""
+    import torch
+    frames, desc = T.make_batch(cfg, N, threads=16)
+    f = torch.from_numpy(frames).cuda()
+    d = torch.from_numpy(desc.view(np.int64)).cuda()
+    crec, pool, cnt = _run_compact(torch, f, d)
+    assert int(cnt[nsd.CNT_PKTS]) == N and int(cnt[nsd.CNT_OVERFLOW]) == 0
+
+    rng = np.random.default_rng(cfg + 100)
+    idx = np.unique(np.concatenate([rng.integers(0, N, 1 << 16), np.arange(4096), np.arange(N - 4096, N)]))
+    orec, oext, _, _ = T.oracle_records(frames, desc[idx])
+    want, _ = nsd.compact_of(orec, oext)
+    got = crec[idx]
+    for fld in ("ip_csum", "nflags", "nlayers"):
+        bad = np.nonzero(got[fld] != want[fld])[0]
+        assert len(bad) == 0, f"{fld} differs at packets {idx[bad[:10]]}"
+    inline = (want["nflags"] & 7) != 7
+    assert np.array_equal(got["chain"][inline], want["chain"][inline])
+    for k in np.nonzero(~inline)[0]:
+        assert _cids(crec, pool, int(idx[k])) == _chain(orec, oext, int(k))[0], f"chain differs at {idx[k]}"
+
+    # determinism (entries may land in other pool slots)
+    crec2, pool2, cnt2 = _run_compact(torch, f, d)
+    assert np.array_equal(cnt2, cnt)
+    for fld in ("ip_csum", "nflags", "nlayers"):
+        assert np.array_equal(crec2[fld], crec[fld]), fld
+    deep = ((crec["nflags"] & 7) == 7) & (crec["nlayers"] == 0)
+    assert np.array_equal(crec2["chain"][~deep], crec["chain"][~deep])
+    side = ((crec["nflags"] & 7) == 7) & (crec["nlayers"] > 0)
+    assert np.array_equal(pool2[:N][side], pool[:N][side])
+    for i in np.nonzero(deep)[0]:
+        assert _cids(crec2, pool2, int(i)) == _cids(crec, pool, int(i))
+
+    # two half batches = the whole (what the multi-GPU shards rely on)
+    h = N // 2
+    ca, pa, na = _run_compact(torch, f, d[:h])
+    cb, pb, nb = _run_compact(torch, f, d[h:])
+    assert np.array_equal(na + nb, cnt)
+    for fld in ("ip_csum", "nflags", "nlayers"):
+        assert np.array_equal(np.concatenate([ca[fld], cb[fld]]), crec[fld]), fld
+    cat = np.concatenate([ca["chain"], cb["chain"]])
+    assert np.array_equal(cat[~deep], crec["chain"][~deep])
+    assert np.array_equal(np.concatenate([pa[:h], pb[:N - h]])[side], pool[:N][side])
+    for i in np.nonzero(deep)[0]:
+        i = int(i)
+        half = _cids(ca, pa, i) if i < h else _cids(cb, pb, i - h)
+        assert half == _cids(crec, pool, i)
+
+    # counters = the tally over every chain
+    assert np.array_equal(cnt[:32], _compact_ops(crec, pool))

@@ -1,53 +1,64 @@
-"""world_size-2 gloo test of the multi-GPU design on CPU: contiguous shards
-cover the batch exactly once, and all-reducing the per-rank counter vectors
-gives the counters of the whole batch (counters computed per shard by the CPU
-oracle standing in for each rank's device)."""
+"""world_size-2 gloo tests of the multi-GPU path on CPU.
+
+test_bench_rank_body runs bench.py's own per-rank body (bench.measure_rank:
+weak shards from nsd_dist.weak_shard, barrier + timed steps, the counter
+all-reduce nsd_dist.reduce_counters inside the timed region, times maxed by
+nsd_dist.max_over_ranks, the counter check) with each rank's shard walked by
+the product's host walk (nsd.walk_cpu -> nsd_walk_packet_cpu) in place of
+the kernel; the summed counters must equal the CPU oracle's over the whole
+job, times the step count.  test_spawn_refuses_missing_gpus checks that
+`bench.py --gpus N` without a launcher fails non-zero when fewer than N GPUs
+are visible (here: none), before touching any."""
 import os
-import socket
+import subprocess
+import sys
 
 import numpy as np
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import nsd_dist
 import nsd_testlib as T
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, total, cfg, out):
+def _worker(rank, world, port, key, per_rank, steps, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    lo, hi = nsd_dist.shard_range(total, rank, world)
-    frames, desc = T.make_batch(cfg, hi - lo, lo=lo)
-    _, _, cnt, _ = T.oracle_records(frames, desc)
-    c = torch.from_numpy(cnt.view(np.int64).copy())
-    nsd_dist.reduce_counters(c)
-    m = nsd_dist.max_over_ranks([float(rank)], "cpu")
-    if rank == 0:
-        np.save(out, c.numpy())
-        assert m == [float(world - 1)]
+    os.environ["RANK"], os.environ["WORLD_SIZE"], os.environ["LOCAL_RANK"] = str(rank), str(world), str(rank)
+    sys.path.insert(0, ROOT)
+    import bench
+    nsd_dist.init("gloo")
+    r, w, _ = nsd_dist.rank_env()
+    args = bench.parse_args(["--gpus", str(w), "--config", key, "--packets", str(per_rank), "--steps", str(steps),
+                             "--warmup", "1"])
+    _, m = bench.measure_rank(args, r, w, "cpu", engine="host")
+    if r == 0:
+        np.save(out, np.concatenate([m["counters"].view(np.int64), [m["total_pkts"]]]))
     dist.destroy_process_group()
 
 
-def test_sharded_counters_allreduce(tmp_path):
-    world, total = 2, 40000
-    for cfg in (T.SYN_IMIX, T.SYN_IPV6X):
-        out = str(tmp_path / f"c{cfg}.npy")
-        mp.spawn(_worker, args=(world, _free_port(), total, cfg, out), nprocs=world, join=True)
-        got = np.load(out).view(np.uint64)
-        frames, desc = T.make_batch(cfg, total)
+def test_bench_rank_body(tmp_path):
+    world, per_rank, steps = 2, 6000, 2
+    for key, cfg in (("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):
+        out = str(tmp_path / f"{key}.npy")
+        mp.spawn(_worker, args=(world, nsd_dist.free_port(), key, per_rank, steps, out), nprocs=world, join=True)
+        res = np.load(out)
+        got, total = res[:-1].view(np.uint64), int(res[-1])
+        assert total == world * per_rank
+        frames, desc = T.make_batch(cfg, world * per_rank)          # both ranks' shards
         _, _, want, _ = T.oracle_records(frames, desc)
-        assert np.array_equal(got, want)
-        assert int(got[32]) == total
+        assert np.array_equal(got, want * np.uint64(steps))
+        assert int(got[32]) == world * per_rank * steps
+
+
+def test_spawn_refuses_missing_gpus():
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    assert r.returncode == 2 and b"GPU(s) visible" in r.stderr
 
 
 def test_shards_partition_exactly():
