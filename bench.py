@@ -322,14 +322,22 @@ def pmc_traffic(args, keys, steps=3):
             for fn in files:
                 with open(fn) as f:
                     for j, row in enumerate(csv.DictReader(f)):
-                        if "dissect_all" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                        if "nsd::dissect_" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
                             order = row.get("Dispatch_Id") or row.get("Correlation_Id") or j
-                            rows.append((int(order), float(row["Counter_Value"])))
+                            rows.append((int(order), row["Kernel_Name"], float(row["Counter_Value"])))
             rows.sort()
-            if len(rows) != steps * len(keys):
-                return {"error": f"{ctr}: {len(rows)} dissect dispatches, expected {steps * len(keys)}"}
+            # one launch = dissect_fast + the dissect_walk after it (the split
+            # schedule), or one dissect_all (the fused kernel)
+            launches = []
+            for _, name, v in rows:
+                if "dissect_walk" in name and launches:
+                    launches[-1] += v
+                else:
+                    launches.append(v)
+            if len(launches) != steps * len(keys):
+                return {"error": f"{ctr}: {len(launches)} dissect launches, expected {steps * len(keys)}"}
             for i, key in enumerate(keys):
-                v = [x for _, x in rows[i * steps:(i + 1) * steps]]
+                v = launches[i * steps:(i + 1) * steps]
                 got.setdefault(key, {})[ctr] = sum(v) / len(v) * 1024
     out = {}
     for key in keys:
@@ -382,20 +390,30 @@ def cpu_rate(cfg, n_sample, threads, seconds, text):
 
 
 def cpu_baseline(key, seconds):
+    """The CPU restatement on this host (SURVEY 8d / BASELINE.md "CPU-baseline
+    plan"): fields + PRINT_NORM text and fields only, each on 1 thread, on
+    the GPU's 16-thread CPU share and on every available core.  `value` is
+    the text rate on all available cores (what the reference does - it
+    prints as it parses - on the whole host), `cores` that thread count."""
     cfg = CONFIGS[key]["cfg"]
     model, nproc, avail = cpu_info()
-    threads = min(avail, 16)   # the GPU box's CPU share per GPU is 16 threads
-    t1, p1, d1 = cpu_rate(cfg, 1 << 16, 1, seconds / 4, True)
-    tN, pN, dN = cpu_rate(cfg, 1 << 20, threads, seconds / 4, True)
-    f1, q1, e1 = cpu_rate(cfg, 1 << 20, 1, seconds / 4, False)
-    fN, qN, eN = cpu_rate(cfg, 1 << 22, threads, seconds / 4, False)
-    return {"value": round(tN, 3), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+    t16 = min(avail, 16)   # the GPU box's CPU share per GPU is 16 threads
+    legs = 6
+    t1, p1, d1 = cpu_rate(cfg, 1 << 16, 1, seconds / legs, True)
+    tS, pS, dS = cpu_rate(cfg, 1 << 20, t16, seconds / legs, True)
+    tA, pA, dA = cpu_rate(cfg, max(1 << 20, 4096 * avail), avail, seconds / legs, True)
+    f1, q1, e1 = cpu_rate(cfg, 1 << 20, 1, seconds / legs, False)
+    fS, qS, eS = cpu_rate(cfg, 1 << 22, t16, seconds / legs, False)
+    fA, qA, eA = cpu_rate(cfg, max(1 << 22, 65536 * avail), avail, seconds / legs, False)
+    return {"value": round(tA, 3), "unit": "Mpkt/s", "cores": avail, "kind": "port",
             "sample": f"{key}: fields + PRINT_NORM text (the reference prints as it parses) by the CPU "
-                      f"restatement (oracle/nsd_oracle.c), {threads} threads over contiguous shards, "
-                      f"{pN} packets (passes over a resident 1M-packet sample) in {dN:.1f} s",
+                      f"restatement (oracle/nsd_oracle.c), {avail} threads (every available core) over "
+                      f"contiguous shards, {pA} packets (passes over a resident "
+                      f"{max(1 << 20, 4096 * avail)}-packet sample) in {dA:.1f} s",
             "cpu_model": model, "nproc": nproc, "cpus_available": avail,
             "text_1thread": round(t1, 3),
-            "fields_only": {"threads": round(fN, 3), "1thread": round(f1, 3)},
+            "text_16threads": {"threads": t16, "value": round(tS, 3)},
+            "fields_only": {"all_cores": round(fA, 3), "threads16": round(fS, 3), "1thread": round(f1, 3)},
             "reference_harness_container": "0.182 Mpkt/s PRINT_NORM 1 core (BASELINE.md, measured in the "
                                            "build container, not on this host)"}
 
@@ -442,14 +460,15 @@ def bpf_bench(b, steps, warmup):
 def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
     """Host memory in, records in host memory out: `nbatch`
     batches of `batch` packets from one pinned host buffer go through the
-    pipelined path (nsd_pipe_*: H2D, dissect kernels, D2H of records, ext and
-    counters, `depth` batches in flight)."""
+    pipelined path (nsd_pipe_*, compact records: H2D, dissect kernels, D2H of
+    records, counters and - when a record needs them - side words / ext
+    entries, `depth` batches in flight)."""
     L = nsd.lib()
     n = batch * nbatch
     frames, desc = T.make_batch(cfg, n, lo=0, threads=16)
     off = (desc & np.uint64((1 << 40) - 1)).astype(np.int64)
     cap = (desc >> np.uint64(40)).astype(np.int64)
-    rec = np.zeros(n, dtype=nsd.REC_DTYPE)
+    rec = np.zeros(n, dtype=nsd.CREC_DTYPE)
     pinned = [a for a in (frames, rec) if L.nsd_host_register(a.ctypes.data, a.nbytes) == 0]
     slices = []
     for k in range(nbatch):
@@ -459,8 +478,8 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
         slices.append((frames[lo:hi + nsd.FRAME_PAD], d, rec[a:b]))
     descs_pinned = [L.nsd_host_register(d.ctypes.data, d.nbytes) == 0 for _, d, _ in slices]
     max_bytes = max(f.nbytes for f, _, _ in slices)
-    ext_w = nsd.ext_pool_words(batch) if cfg == T.SYN_IPV6X else nsd.ext_pool_words(batch // 64)
-    pipe = nsd.Pipe(batch, max_bytes, ext_words=ext_w, depth=depth, mode=mode)
+    ext_w = batch + (nsd.ext_pool_words(batch) if cfg == T.SYN_IPV6X else nsd.ext_pool_words(batch // 64))
+    pipe = nsd.Pipe(batch, max_bytes, ext_words=ext_w, depth=depth, mode=mode, compact=True)
     exts = [np.zeros(ext_w, dtype=np.uint32) for _ in range(depth + 1)]
     cnts = np.zeros((nbatch, nsd.NCOUNTERS), np.uint64)
     ecs = np.zeros(nbatch, np.uint32)
@@ -477,7 +496,7 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
     pipe.close()
     assert int(cnts[:, nsd.CNT_PKTS].sum()) == n and not sts.any()
     h2d = sum(f.nbytes - nsd.FRAME_PAD + d.nbytes for f, d, _ in slices)
-    d2h = n * REC_B
+    d2h = n * CREC_B
     dt = min(times)
     for a in pinned:
         L.nsd_host_unregister(a.ctypes.data)
@@ -486,36 +505,47 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
             L.nsd_host_unregister(d.ctypes.data)
     return {"value": round(n / dt / 1e6, 2), "unit": "Mpkt/s",
             "pcie_gbs": round((h2d + d2h) / dt / 1e9, 2),
-            "h2d_bytes_per_pkt": round(h2d / n, 2), "d2h_bytes_per_pkt": REC_B,
+            "h2d_bytes_per_pkt": round(h2d / n, 2), "d2h_bytes_per_pkt": CREC_B,
+            "records": "compact 8 B (nsd_crec)",
             "batches": nbatch, "batch_packets": batch, "depth": depth,
             "pinned": len(pinned) == 2 and all(descs_pinned),
-            "note": "host frames -> H2D -> dissect kernels -> D2H records/ext/counters "
-                    "(nsd_pipe_*), best of %d passes" % reps}
+            "note": "host frames -> H2D -> dissect kernels -> D2H records/counters "
+                    "(nsd_pipe_*, compact records), best of %d passes" % reps}
 
 
 def replay_leg(cfg, n, mode, threads, reps=2):
     """`netsniff-ng --in file.pcap` through the device (nsd_replay_pcap): a
     synthetic pcap of n records in a temp file -> reader -> pipelined device
-    walk -> host formatter on `threads` threads -> /dev/null."""
+    walk (compact records) -> host formatter pool of `threads` threads ->
+    /dev/null; and the same with one formatter thread over n/8 records (the
+    product formatter's single-thread rate, beside cpu_baseline.text_1thread)."""
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "replay.pcap")
         T.synth().nsd_synth_pcap(cfg, T.SEED, 0, n, path.encode())
+        path1 = os.path.join(d, "replay1.pcap")
+        n1 = max(n // 8, 1)
+        T.synth().nsd_synth_pcap(cfg, T.SEED, 0, n1, path1.encode())
         size = os.path.getsize(path)
         fd = os.open(os.devnull, os.O_WRONLY)
         try:
-            best = None
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                got, _ = nsd.replay_pcap(path, mode=mode, threads=threads, out_fd=fd)
-                dt = time.perf_counter() - t0
-                assert got == n
-                best = dt if best is None else min(best, dt)
+            def best_of(pth, cnt, th):
+                best = None
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    got, _ = nsd.replay_pcap(pth, mode=mode, threads=th, out_fd=fd)
+                    dt = time.perf_counter() - t0
+                    assert got == cnt
+                    best = dt if best is None else min(best, dt)
+                return best
+            best = best_of(path, n, threads)
+            best1 = best_of(path1, n1, 1)
         finally:
             os.close(fd)
     return {"value": round(n / best / 1e6, 3), "unit": "Mpkt/s", "packets": n,
             "file_gbs": round(size / best / 1e9, 2), "format_threads": threads,
-            "note": "pcap file -> nsd_pcap reader -> H2D -> dissect kernels -> D2H -> host text "
-                    "formatter -> /dev/null (nsd_replay_pcap), best of %d" % reps}
+            "format_1thread": round(n1 / best1 / 1e6, 3),
+            "note": "pcap file -> nsd_pcap reader -> H2D -> dissect kernels -> D2H compact records -> "
+                    "formatter pool -> writev /dev/null (nsd_replay_pcap), best of %d" % reps}
 
 
 def copy_rate(dev):
@@ -606,7 +636,7 @@ def parse_args(argv=None):
     ap.add_argument("--records", default="compact", choices=["compact", "full"],
                     help="record form of the timed launches: 8-byte nsd_crec or 16-byte nsd_rec")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline duration (all legs)")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU baseline duration (all legs)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end pass")
     ap.add_argument("--no-bpf", action="store_true", help="skip the device BPF filter pass")
     ap.add_argument("--no-replay", action="store_true", help="skip the pcap replay (--in) pass")
@@ -704,6 +734,10 @@ def main():
     replay = None
     if solo and not args.no_replay:
         replay = replay_leg(CONFIGS[args.config]["cfg"], args.replay_packets, args.mode, min(cpu_info()[2], 16))
+        if cpu is not None:
+            # the CPU-only text rate on the same thread count
+            replay["cpu_text_same_threads"] = cpu["text_16threads"]["value"]
+            replay["vs_cpu_text_same_threads"] = round(replay["value"] / cpu["text_16threads"]["value"], 3)
 
     if rank == 0:
         out = {

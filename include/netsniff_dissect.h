@@ -180,6 +180,8 @@ enum nsd_counter {
 #define NSD_ERR_CAPLEN      -3
 #define NSD_ERR_NOMEM       -4
 #define NSD_ERR_FORMAT      -5
+#define NSD_ERR_UNSUPPORTED -6   /* a chain reaches a reference object (802.11 / netlink)
+                                    that prints through tprintf (pcap replay) */
 
 /* ---- reference surface (dissector.h:118-122) ----------------------------
  * The per-packet entry runs on the host CPU, as SURVEY 8b plans it (one
@@ -423,11 +425,48 @@ int nsd_dissect_device_compact(const uint8_t *d_frames, const nsd_desc_t *d_desc
 			       void *stream);
 /* nsd_format_batch_sll over compact records: each layer starts where the
  * previous one's print left the cursor.  A record without its chain (NSD_F_OVERFLOW)
- * gets rc NSD_ERR_FORMAT (render it per packet: dissector_entry_point). */
+ * gets rc NSD_ERR_FORMAT (render it per packet: dissector_entry_point).
+ * Packet i's side word is ext_pool[i]: the call covers a whole launch's
+ * batch (for a part of one: nsd_format_range_compact). */
 long nsd_format_batch_compact(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
 			      uint32_t n, int linktype, int mode, const nsd_crec *crec,
 			      const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends,
 			      int8_t *rc);
+
+/* Kernel schedule of the batch walks.  NSD_SCHED_SPLIT: a fast kernel
+ * (fast walk of every packet at high occupancy) plus a walker kernel over
+ * the packets it defers; NSD_SCHED_FUSED: one kernel doing both; results
+ * are identical.  NSD_SCHED_ADAPTIVE (the default) picks per device from the
+ * recently observed share of deferred packets (split for traffic the fast
+ * walk finishes, fused for deep chains).  nsd_set_schedule returns the
+ * previous setting (or NSD_ERR_ARG); nsd_last_schedule the schedule of the
+ * last launch (NSD_SCHED_SPLIT / _FUSED, 0 before any). */
+#define NSD_SCHED_ADAPTIVE 0
+#define NSD_SCHED_SPLIT    1
+#define NSD_SCHED_FUSED    2
+int nsd_set_schedule(int sched);
+int nsd_last_schedule(void);
+
+/* Compact-record pipe: nsd_pipe_create_compact as nsd_pipe_create, its
+ * batches walked into nsd_crec records.  The pool needs ext_words >=
+ * max_pkts + the entries (its words [0, n) are the batch's side words).
+ * nsd_pipe_submit_compact as nsd_pipe_submit_sll with crec[n]: ext[0, n +
+ * *ext_used) receives the side words and the entries only when a record of
+ * the batch needs either (its counters[NSD_CNT_EXT] > 0; otherwise ext is
+ * left as it was).  Each submit form refuses the other kind of pipe. */
+nsd_pipe *nsd_pipe_create_compact(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_words,
+				  int depth, int linktype, int mode);
+int nsd_pipe_submit_compact(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
+			    const nsd_desc_t *desc, const nsd_sll_t *sll, uint32_t n, nsd_crec *crec,
+			    uint32_t *ext, uint32_t *ext_used, uint64_t *counters, int *status);
+/* nsd_format_batch_compact over packets [lo, hi) of a launch's batch: desc,
+ * sll (may be NULL) and crec are the whole batch's arrays and ext_pool its
+ * pool, so a range's side words are found at their batch index (what lets
+ * a caller split one batch over threads; nsd_format_batch_compact itself
+ * must be given the whole batch).  ends[k - lo] / rc[k - lo] per packet. */
+long nsd_format_range_compact(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+			      uint32_t lo, uint32_t hi, int linktype, int mode, const nsd_crec *crec,
+			      const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends, int8_t *rc);
 
 /* ---- pcap replay front end (`netsniff-ng --in f.pcap`, read_pcap
  * netsniff-ng.c:640-770; pcap_io.h / pcap_sg.c record formats) ---------------

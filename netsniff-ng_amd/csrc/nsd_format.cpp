@@ -1220,18 +1220,25 @@ extern "C" long nsd_format_batch_compact(const uint8_t *frames, const nsd_desc_t
 					 const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends,
 					 int8_t *rc)
 {
-	if (n && (!frames || !desc || !crec))
+	return nsd_format_range_compact(frames, desc, sll, 0, n, linktype, mode, crec, ext_pool, out, cap, ends, rc);
+}
+
+extern "C" long nsd_format_range_compact(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+					 uint32_t lo, uint32_t hi, int linktype, int mode, const nsd_crec *crec,
+					 const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends, int8_t *rc)
+{
+	if (hi < lo || (hi > lo && (!frames || !desc || !crec)))
 		return NSD_ERR_ARG;
 	std::string s;
 	s.reserve(cap ? cap : 4096);
-	for (uint32_t i = 0; i < n; i++) {
+	for (uint32_t i = lo; i < hi; i++) {
 		const uint64_t d = desc[i];
 		int r = nsd::format_packet_compact(s, frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), linktype, mode,
 						   crec[i], i, ext_pool, sll ? sll + i : nullptr);
 		if (rc)
-			rc[i] = (int8_t)r;
+			rc[i - lo] = (int8_t)r;
 		if (ends)
-			ends[i] = s.size();
+			ends[i - lo] = s.size();
 	}
 	if (s.size() > cap)
 		return -(long)s.size();

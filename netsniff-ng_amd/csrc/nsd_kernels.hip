@@ -28,12 +28,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "nsd_walk.h"
 
 namespace nsd {
 
 constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
+
+// Packets the fast walk handed to the general walk, summed over launches on
+// this device: the launcher samples it now and then to choose the schedule
+// (split or fused, nsd_launch_dissect_rec)
+__device__ unsigned long long g_deferred;
 constexpr int WIN1 = 64;         // bytes per staged window, pass 1
 #ifndef NSD_WIN2
 #define NSD_WIN2 128
@@ -77,8 +84,9 @@ struct HbmBytes {
 };
 
 // Byte source over an LDS window (aligned coordinates, see top).
-// FAST (the fast walk): the window is a zero-padded 20-dword row (bytes past
-// caplen zeroed by stage_write); bytes outside it are not fetched, the
+// FAST (the fast walk): the window is a zero-padded row (bytes past caplen
+// zeroed by stage_write; 20-dword rows, or the split schedule's 16-dword rows
+// with their 16-byte slots XOR-swizzled by sw); bytes outside it are not fetched, the
 // source records the miss and the walk gives the packet up to the general
 // walk.  Otherwise (the general walk's continuation windows, stage_glds): a
 // row of WIN bytes filled by LDS-DMA with its 16-byte slots XOR-swizzled
@@ -96,7 +104,7 @@ struct LSrc {
 	mutable bool miss;
 	uint32_t sw;             // continuation rows: slot swizzle (dword index xor)
 
-	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return FAST ? win[j] : win[j ^ sw]; }
+	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return win[j ^ sw]; }
 	__device__ __forceinline__ int lay3(uint32_t key) const { return lay3t[key & 255]; }
 	__device__ __forceinline__ uint32_t step(int id) const { return stept[id & 31]; }
 	__device__ __forceinline__ uint32_t l2h(uint32_t h) const { return stept[32 + (h & 31)]; }
@@ -165,6 +173,12 @@ struct LSrc {
 	{
 		const uint32_t r = o + m - wb;
 		return r < WIN && r + nbytes <= WIN;
+	}
+	// window bytes from frame offset o to the window's end
+	__device__ __forceinline__ uint32_t window_bytes(uint32_t o) const
+	{
+		const uint32_t r = o + m - wb;
+		return r < WIN ? WIN - r : 0u;
 	}
 	// the next layer would read past the staged window (the bytes its parse
 	// inspects from its start, c_step's `need`): general walk only
@@ -744,6 +758,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	const GenSink<CR> g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.ops, &sh.lay[wv][0],
 			 side ? n : 0u, side ? ext : nullptr };
 	FlagCnt fc;
+	uint32_t ndefer = 0;
 	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
 
 	if (MODE != PRINT_NORM && MODE != PRINT_LESS) {
@@ -809,6 +824,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 				fw = fast_walk<MODE>(src, caplen, w);
 			}
 			deferred = fw != FW_DONE;
+			ndefer += FlagCnt::pc(deferred);
 			wave_sync_lds();
 			const bool done = valid && !deferred;
 			if (MODE == PRINT_NORM) {
@@ -893,6 +909,8 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 		d1 = d2;
 	}
 	fc.flush(s_cnt, lane);
+	if (lane == 0 && ndefer)
+		atomicAdd(&g_deferred, (unsigned long long)ndefer);
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
@@ -1037,6 +1055,473 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 }
 
 
+// ==== the split schedule ===========================================================
+// Two launches per batch.  dissect_fast runs the fast walk of every tile at
+// high occupancy (8 waves per SIMD: its registers and LDS are only what the
+// fast walk needs), writes the records of the packets it finishes, sums the
+// ICMPv4 messages they leave pending and appends every packet it cannot
+// finish to its wave's deferral list; dissect_walk runs the walker pool
+// (walkers(), the general walk) over those lists.  The fused kernel's
+// register peak is the walker pool's (119 VGPRs: 4 waves per SIMD), which
+// C2 and C3 - nearly nothing deferred - paid for in latency hiding.
+//
+// A fast wave's list (`cap` slots of 32 bytes):
+//   deferrals from the front: { packet, data | tail << 16,
+//     ip_csum | flags << 16 | n << 24 | id << 27, chain },
+//     { descriptor, starts of layers 1..4 (a byte each: the fast window) }
+//   pending ICMPv4 checksums from the back: { packet, off | len << 16,
+//     the message's words before off, summed and weighted like the pass
+//     (below) }, { descriptor }
+// and its counts at cnts[wave] = { deferrals, checksums }.  The descriptor
+// rides along so the walker kernel and the checksum pass read no desc[]
+// (and the walker kernel knows the next chunk's window addresses early).
+
+constexpr int FROW = WIN1 / 4;   // fast rows: 16 dwords, 16-byte slots XOR-swizzled by swz_of(q, 4)
+#ifndef NSD_FAST_MINW
+#define NSD_FAST_MINW 6          // waves per SIMD dissect_fast is register-allocated for
+#endif
+#ifndef NSD_FAST_PREF
+#define NSD_FAST_PREF 2          // where the next tile's chunk loads are issued (fast_tiles)
+#endif
+#ifndef NSD_FAST_CSUM_U
+#define NSD_FAST_CSUM_U 4        // interior chunk loads in flight per lane (fast_icmp_pass)
+#endif
+
+struct FastShared {
+	alignas(16) uint32_t win[WAVES][64 * FROW];   // fast rows
+	unsigned long long cnt[NSD_NCOUNTERS];        // block counters
+	uint32_t ops[32];                             // block per-ops layer counts
+	uint8_t lay3[256];                            // eth_lay3
+	uint32_t pcnt[WAVES];                         // pending checksums per wave
+};
+
+// stage_write into the split schedule's rows: chunk c of packet q at slot
+// c ^ swz(q) of its 16-dword row (ds_write_b128; the 8 lanes of a store
+// group cover two whole rows: no bank conflict)
+__device__ __forceinline__ void stage_write_sw(uint32_t *wwin, const Chunks<WIN1> &ch, int lane)
+{
+#pragma unroll
+	for (int r = 0; r < 4; r++) {
+		const int t = r * 64 + lane;
+		const int q = t / 4, c = t % 4;
+		const uint32_t nv = (ch.nv >> (8 * r)) & 0xFF;
+		uint32_t w[4] = { ch.v[r].x, ch.v[r].y, ch.v[r].z, ch.v[r].w };
+		if (nv < 16) {
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				const uint32_t bp = 4 * j;
+				if (bp >= nv)
+					w[j] = 0;
+				else if (bp + 4 > nv)
+					w[j] &= (1u << ((nv - bp) * 8)) - 1u;
+			}
+		}
+		*(uint4 *)(wwin + q * FROW + ((c ^ swz_of((uint32_t)q, 4)) << 2)) = make_uint4(w[0], w[1], w[2], w[3]);
+	}
+}
+
+// a folded 16-bit partial sum in the pass's byte weighting: the pass sums a
+// message's bytes as aligned little-endian halves, which weights them by 256
+// (mod 0xFFFF) against the reference's words when the message starts at an
+// odd address (see the ICMPv4 checksum helpers above); so is the partial
+__device__ __forceinline__ uint32_t fold_weighted(uint32_t sum, bool odd)
+{
+	sum = (sum >> 16) + (sum & 0xFFFF);
+	sum = (sum >> 16) + (sum & 0xFFFF);
+	return odd ? ((sum & 0xFF) << 8 | sum >> 8) : sum;
+}
+
+template <int MODE, bool CR>
+__device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__restrict__ frames,
+					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
+					   void *__restrict__ rec, const uint32_t *__restrict__ sll, uint4 *__restrict__ list,
+					   uint32_t cap, uint32_t &ndef, uint32_t &nicmp)
+{
+	constexpr int SW = 2;
+	const int lane = threadIdx.x & 63;
+	const int wv = threadIdx.x >> 6;
+	const uint32_t stride = gridDim.x * BLOCK;
+	FlagCnt fc;
+	uint32_t base = blockIdx.x * BLOCK + wv * 64;
+
+	if (MODE != PRINT_NORM && MODE != PRINT_LESS) {
+		// every process() is NULL: no chain (dissector.c:51-53)
+		for (; base < n; base += stride) {
+			const uint32_t i = base + lane;
+			fc.pkts += FlagCnt::pc(i < n);
+			if (i < n) {
+				const uint32_t caplen = NSD_DESC_CAPLEN(desc[i]);
+				if constexpr (CR)
+					__builtin_nontemporal_store(v2u{ 0u, 0u }, (v2u *)rec + i);
+				else
+					store_rec((uint4 *)rec, i, make_uint4(0, caplen << 16, 0, 0));
+				fc.bytes += caplen;
+			}
+		}
+		fc.flush(sh.cnt, lane);
+		return;
+	}
+	if (base >= n)
+		return;
+	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
+	// descriptors are in flight
+	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
+	uint64_t d1 = (base + stride < n && base + stride + lane < n) ? desc[base + stride + lane] : 0;
+	Chunks<WIN1> ch;
+	stage_load<WIN1>(ch, frames, d0, lane);
+	uint32_t *const rows = &sh.win[wv][0];
+	for (; base < n; base += stride) {
+		const uint32_t i = base + lane;
+		const bool valid = i < n;
+		const uint64_t off = NSD_DESC_OFF(d0);
+		const uint32_t caplen = NSD_DESC_CAPLEN(d0);
+		WalkOut w;
+		walk_init(w, caplen, valid ? start_id : 0);
+		stage_write_sw(rows, ch, lane);
+		const uint32_t b2 = base + 2 * stride;
+		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
+		// the next tile's chunk loads: before this tile's walk (in flight
+		// during it; its registers live across the walk), after the walk, or
+		// after the whole tile (NSD_FAST_PREF 2 / 1 / 0)
+		if (NSD_FAST_PREF == 2 && base + stride < n)
+			stage_load<WIN1>(ch, frames, d1, lane);
+		wave_sync_lds();
+		uint32_t fw = FW_DONE;
+		if (valid) {
+			const LSrc<true, WIN1> src{ rows + lane * FROW, sh.lay3, nullptr, frames + off, caplen,
+						    (uint32_t)off & 15, 0, false, swz_of((uint32_t)lane, 4) << 2 };
+			fw = fast_walk<MODE, true>(src, caplen, w);
+		}
+		const bool deferred = fw != FW_DONE;
+		wave_sync_lds();
+		if (NSD_FAST_PREF == 1 && base + stride < n)
+			stage_load<WIN1>(ch, frames, d1, lane);
+		const bool done = valid && !deferred;
+		if (MODE == PRINT_NORM) {
+			// ICMPv4 messages past the window, from the back of the list
+			const bool pnd = w.icmp_pend && done;
+			const uint64_t pm = __ballot(pnd);
+			if (pnd) {
+				const uint32_t part = fold_weighted(w.icmp_sum, ((uint32_t)off + w.icmp_off) & 1);
+				uint4 *e = list + (size_t)(cap - 1 - (nicmp + lanes_below(pm))) * SW;
+				e[0] = make_uint4(i, w.icmp_off | w.icmp_len << 16, part, 0);
+				e[1] = make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), 0, 0);
+			}
+			nicmp += (uint32_t)__popcll(pm);
+		}
+		// per-ops counts of the finished chains, grouped by chain word (as
+		// walk_tiles)
+		{
+			uint32_t key = done ? w.chain : 0xFFFFFFFFu;
+			for (int it = 0;; it++) {
+				const uint64_t pm = __ballot(key != 0xFFFFFFFFu);
+				if (!pm)
+					break;
+				if (it == 2) {
+					if (key != 0xFFFFFFFFu)
+						for (uint32_t k = 0; k < w.n; k++)
+							atomicAdd(&sh.ops[(key >> (5 * k)) & 31], 1u);
+					break;
+				}
+				const int leader = __ffsll((unsigned long long)pm) - 1;
+				const uint32_t lk = __shfl(key, leader, 64);
+				const uint64_t m = __ballot(key == lk);
+				if (lane == leader) {
+					const uint32_t cnt = (uint32_t)__popcll(m);
+					for (uint32_t k = 0, nl = w.n; k < nl; k++)
+						atomicAdd(&sh.ops[(lk >> (5 * k)) & 31], cnt);
+				}
+				if (key == lk)
+					key = 0xFFFFFFFFu;
+			}
+		}
+		if (done)
+			put_rec<CR>(rec, i, w);
+		fc.add(w, caplen, done);
+		// the deferred packets' walk state, for dissect_walk: from the start
+		// (FW_RESTART; the SLL head is run here) or where the fast walk stopped
+		// (FW_RESUME: its layers are counted here)
+		const uint64_t dm = __ballot(deferred);
+		if (dm) {
+			if (deferred) {
+				if (fw == FW_RESTART) {
+					walk_init(w, caplen, start_id);
+					if (start_id == NSD_OPS_SLL) {
+						const uint32_t w0 = sll ? sll[5 * (size_t)i] : 0u;
+						const uint32_t w2 = sll ? sll[5 * (size_t)i + 2] : 0u;
+						const uint32_t proto = __builtin_bswap16((uint16_t)(w0 >> 16));
+						w.chain = NSD_OPS_SLL;
+						w.n = 1;
+						atomicAdd(&sh.ops[NSD_OPS_SLL], 1u);
+						w.id = sll_next(w2 & 0xFFFF, proto, MODE, c_lay2h.e[NSD_L2H(proto)]);
+					}
+				} else {
+					for (uint32_t k = 0; k < w.n; k++)
+						atomicAdd(&sh.ops[(w.chain >> (5 * k)) & 31], 1u);
+				}
+				// (n < 8 and id < 32: a deferred chain holds at most the SLL
+				// head, Ethernet, 2 tags and IP, layer 0 at 0 and the others
+				// inside the 64-byte window)
+				uint4 *e = list + (size_t)(ndef + lanes_below(dm)) * SW;
+				e[0] = make_uint4(i, w.data | w.tail << 16,
+						  (uint32_t)w.ip_csum | (uint32_t)w.flags << 16 | w.n << 24 | (uint32_t)w.id << 27,
+						  w.chain);
+				const uint32_t offs = CR ? 0u
+							 : ((uint32_t)(w.offA >> 16) & 0xFF) | ((uint32_t)(w.offA >> 32) & 0xFF) << 8 |
+								   ((uint32_t)(w.offA >> 48) & 0xFF) << 16 | (w.offB & 0xFF) << 24;
+				e[1] = make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), offs, 0);
+			}
+			ndef += (uint32_t)__popcll(dm);
+		}
+		if (NSD_FAST_PREF == 0 && base + stride < n)
+			stage_load<WIN1>(ch, frames, d1, lane);
+		d0 = d1;
+		d1 = d2;
+	}
+	fc.flush(sh.cnt, lane);
+}
+
+// The fast kernel's pending ICMPv4 checksums (fast_tiles' list backs): as
+// icmp_pass, four lanes per message; the remainder [off, off + len) is summed
+// from HBM and the partial sum of the words before it added.
+template <int U, bool CR>
+__device__ __forceinline__ void fast_icmp_pass(FastShared &sh, const uint8_t *__restrict__ frames,
+					       const uint64_t *__restrict__ desc, void *__restrict__ rec,
+					       const uint4 *__restrict__ lists, uint32_t cap)
+{
+	constexpr int SW = 2;
+	const int lane = threadIdx.x & 63;
+	const int wv = threadIdx.x >> 6;
+	const uint32_t sub = lane & 3, grp = lane >> 2;
+	uint32_t bad = 0;
+	for (int l = 0; l < WAVES; l++) {
+		const uint32_t cnt = sh.pcnt[l];
+		const uint4 *list = lists + ((size_t)blockIdx.x * WAVES + l) * cap * SW;
+		for (uint32_t k0 = 64 * ((wv + l) % WAVES); k0 < cnt; k0 += 64 * WAVES) {
+			const bool on = k0 + lane < cnt;
+			const uint4 *ep = list + (size_t)(cap - 1 - (k0 + lane)) * SW;
+			const uint4 e = on ? ep[0] : make_uint4(0, 0, 0, 0);
+			const uint32_t i = e.x;
+			const uint64_t a = (on ? NSD_DESC_OFF((uint64_t)ep[1].y << 32 | ep[1].x) : 0) + (e.y & 0xFFFF);
+			const uint32_t nb = e.y >> 16;
+			for (uint32_t q = 0; q < 64 && k0 + q < cnt; q += 16) {
+				const int src = (int)(q + grp);
+				const uint32_t alo = __shfl((uint32_t)a, src, 64);
+				const uint32_t ahi = __shfl((uint32_t)(a >> 32), src, 64);
+				const uint32_t mnb = __shfl(nb, src, 64);
+				const uint32_t part = __shfl(e.z, src, 64);
+				const bool mon = k0 + (uint32_t)src < cnt;
+				const uint32_t s0 = alo & 15, endb = s0 + mnb;
+				const uint32_t nch = mon ? (endb + 15) >> 4 : 0u;
+				const uint4 *base = (const uint4 *)(frames + ((((uint64_t)ahi << 32) | alo) & ~15ull));
+				uint32_t sum = sub == 0 ? part : 0u;
+				const uint32_t je = sub == 0 ? 0u : nch - 1;
+				if ((sub == 0 && nch > 0) || (sub == 1 && nch > 1))
+					sum += csum_chunk(base[je], 16 * je, s0, endb);
+				for (uint32_t j = 1 + sub; __ballot(j + 1 < nch); j += 4 * U) {
+					uint4 v[U];
+#pragma unroll
+					for (int u = 0; u < U; u++) {
+						const uint32_t jj = j + 4 * u;
+						v[u] = jj + 1 < nch ? base[jj] : make_uint4(0, 0, 0, 0);
+					}
+#pragma unroll
+					for (int u = 0; u < U; u++) {
+						sum = sum_halves(v[u].x, sum);
+						sum = sum_halves(v[u].y, sum);
+						sum = sum_halves(v[u].z, sum);
+						sum = sum_halves(v[u].w, sum);
+					}
+				}
+				sum = (sum >> 16) + (sum & 0xffff);
+				sum += __shfl_xor(sum, 1, 64);
+				sum += __shfl_xor(sum, 2, 64);
+				const uint32_t mi = __shfl(i, src, 64);
+				const bool isbad = mon && sub == 0 && csum_final(sum) != 0;
+				if (isbad) {
+					uint8_t *nf = (uint8_t *)rec + nflags_at<CR>(mi);
+					*nf = *nf | NSD_F_ICMP_BAD;
+				}
+				bad += FlagCnt::pc(isbad);
+			}
+		}
+	}
+	if (lane == 0 && bad)
+		atomicAdd(&sh.cnt[NSD_CNT_ICMP_BAD], (unsigned long long)bad);
+}
+
+template <int MODE, bool CR>
+__global__ __launch_bounds__(BLOCK, NSD_FAST_MINW) void dissect_fast(
+	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
+	void *__restrict__ rec, unsigned long long *__restrict__ counters, uint4 *__restrict__ lists, uint32_t cap,
+	uint2 *__restrict__ cnts, const uint32_t *__restrict__ sll)
+{
+	constexpr int SW = 2;
+	__shared__ FastShared sh;
+	if (threadIdx.x < 32)
+		sh.ops[threadIdx.x] = 0;
+	block_init(sh.cnt, sh.lay3);
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const uint32_t gw = blockIdx.x * WAVES + wv;
+	uint32_t ndef = 0, nicmp = 0;
+	fast_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, sll, lists + (size_t)gw * cap * SW, cap, ndef, nicmp);
+	if (lane == 0) {
+		cnts[gw] = make_uint2(ndef, nicmp);
+		sh.pcnt[wv] = nicmp;
+		if (ndef)
+			atomicAdd(&g_deferred, (unsigned long long)ndef);
+	}
+	if (MODE == PRINT_NORM) {
+		__syncthreads();   // records final, the block's pending lists and counts complete
+		fast_icmp_pass<NSD_FAST_CSUM_U, CR>(sh, frames, desc, rec, lists, cap);
+	}
+	block_flush(sh.cnt, counters);
+	if (threadIdx.x < 32 && sh.ops[threadIdx.x])
+		atomicAdd(&counters[NSD_CNT_OPS + threadIdx.x], (unsigned long long)sh.ops[threadIdx.x]);
+}
+
+// The walker kernel: wave g of the grid takes the fast kernel's lists g,
+// g + W, g + 2W, ... (W = this grid's waves), 64 deferrals (a chunk) at a
+// time, and hands them to its walker pool (walkers()); then, as the fused
+// kernel, the leaves and ICMPv4 checksums its walks left pending (its own
+// lists, `region` / WAVES slots per wave).  Chunk entries are loaded two
+// chunks ahead, and while chunk c's walkers run, the first windows of chunk
+// c + 1 (at each packet's cursor) are touched into L2 by 4-byte LDS-DMA loads
+// (no VGPR waits for them): its sessions then stage from L2.
+template <int MODE, bool CR>
+__global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
+	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n,
+	void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
+	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
+	const uint4 *__restrict__ lists, uint32_t cap, const uint2 *__restrict__ cnts, uint32_t nlists,
+	uint64_t *__restrict__ pend, uint32_t region)
+{
+	constexpr int SW = 2;
+	__shared__ Shared sh;
+	__shared__ uint32_t s_touch[64];   // the L2 touches' LDS-DMA target (never read)
+	{
+		// nothing deferred to this block's waves (the common case of traffic
+		// the fast walk finishes): leave before any set-up
+		const uint32_t nw = gridDim.x * WAVES;
+		bool any = false;
+		for (uint32_t L = blockIdx.x * WAVES + (threadIdx.x % WAVES) + (threadIdx.x / WAVES) * nw; L < nlists;
+		     L += (BLOCK / WAVES) * nw)
+			any = any || cnts[L].x != 0;
+		if (!__syncthreads_or(any))
+			return;
+	}
+	if (threadIdx.x < 64)
+		sh.step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h.e[threadIdx.x - 32];
+	if (threadIdx.x < 32)
+		sh.ops[threadIdx.x] = 0;
+	if (threadIdx.x < 2 * WAVES)
+		sh.wc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+	block_init(sh.cnt, sh.lay3);
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const uint32_t gw = blockIdx.x * WAVES + wv, nw = gridDim.x * WAVES;
+	Pending pq{ pend + (size_t)gw * (region / WAVES), region / WAVES, 0, 0 };
+	const bool side = CR && ext_words >= n;
+	const GenSink<CR> g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.ops, &sh.lay[wv][0],
+			     side ? n : 0u, side ? ext : nullptr };
+	FlagCnt fc;
+	Walker wk;
+	walk_init(wk.w, 0, 0);
+	wk.d = 0;
+	wk.i = 0;
+	wk.wb = 0;
+	wk.have = false;
+	wk.stage = false;
+	WalkOut pw;
+	walk_init(pw, 0, 0);
+
+	// chunk positions (wave-uniform): list L, first entry k0, the list's count
+	struct Pos {
+		uint32_t L, k0, cnt;
+	};
+	auto adv = [&](Pos p) -> Pos {
+		p.k0 += 64;
+		while (p.L < nlists && p.k0 >= p.cnt) {
+			p.L += nw;
+			p.k0 = 0;
+			p.cnt = p.L < nlists ? min(cnts[p.L].x, cap) : 0u;
+		}
+		return p;
+	};
+	auto load = [&](const Pos &p, uint4 &x0, uint4 &x1) {
+		x0 = x1 = make_uint4(0, 0, 0, 0);
+		if (p.L < nlists && p.k0 + lane < p.cnt) {
+			const uint4 *e = lists + ((size_t)p.L * cap + p.k0 + lane) * SW;
+			x0 = e[0];
+			x1 = e[1];
+		}
+	};
+	Pos p0 = adv(Pos{ gw, 0u - 64u, gw < nlists ? min(cnts[gw].x, cap) : 0u });
+	Pos p1 = adv(p0);
+	uint4 c0, c1, n0, n1;
+	load(p0, c0, c1);
+	load(p1, n0, n1);
+	while (p0.L < nlists) {
+		const Pos p2 = adv(p1);
+		{
+			// the next chunk's first windows into L2: [cursor, +WIN2) in aligned
+			// coordinates, one or two 128-byte lines
+			const uint64_t d = (uint64_t)n1.y << 32 | n1.x;
+			const uint32_t m = (uint32_t)NSD_DESC_OFF(d) & 15, caplen = NSD_DESC_CAPLEN(d);
+			const uint32_t wb = ((n0.y & 0xFFFF) + m) & ~15u;
+			const bool on = p1.L < nlists && p1.k0 + lane < p1.cnt && wb < caplen + m;
+			const uint64_t a = (uint64_t)frames + (NSD_DESC_OFF(d) & ~15ull) + wb;
+			const bool two = on && (a & 127) != 0 && wb + (128 - (uint32_t)(a & 127)) < caplen + m;
+			if (on)
+				__builtin_amdgcn_global_load_lds((const void *)(a & ~127ull),
+								 (__attribute__((address_space(3))) void *)s_touch, 4, 0, 0);
+			if (two)
+				__builtin_amdgcn_global_load_lds((const void *)((a & ~127ull) + 128),
+								 (__attribute__((address_space(3))) void *)s_touch, 4, 0, 0);
+		}
+		uint4 m0, m1;
+		load(p2, m0, m1);
+		bool pnd = p0.k0 + lane < p0.cnt;
+		const uint32_t pi = c0.x;
+		const uint64_t pd = (uint64_t)c1.y << 32 | c1.x;
+		walk_init(pw, c0.y >> 16, (int)(c0.z >> 27));
+		pw.data = c0.y & 0xFFFF;
+		pw.ip_csum = (uint16_t)c0.z;
+		pw.flags = (uint8_t)(c0.z >> 16);
+		pw.n = (c0.z >> 24) & 7;
+		pw.chain = c0.w;
+		if (!CR) {
+			// layer starts 1..4 (layer 0 at 0)
+			pw.offA = (uint64_t)(c1.z & 0xFF) << 16 | (uint64_t)((c1.z >> 8) & 0xFF) << 32 |
+				  (uint64_t)((c1.z >> 16) & 0xFF) << 48;
+			pw.offB = c1.z >> 24;
+		}
+		walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, pnd, pw, pi, pd, false);
+		c0 = n0;
+		c1 = n1;
+		n0 = m0;
+		n1 = m1;
+		p0 = p1;
+		p1 = p2;
+	}
+	{
+		bool none = false;
+		if (__ballot(wk.have))
+			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, none, pw, 0, 0, true);
+	}
+	fc.flush(sh.cnt, lane);
+	if (!CR)
+		leaf_pass<MODE>(frames, desc, (uint4 *)rec, pq);
+	if (lane == 0)
+		sh.pcnt[wv] = pq.npend;
+	if (MODE == PRINT_NORM) {
+		__syncthreads();
+		icmp_pass<NSD_CSUM_U, CR>(sh, frames, desc, rec, pend, region);
+	}
+	block_flush(sh.cnt, counters);
+	if (threadIdx.x < 32 && sh.ops[threadIdx.x])
+		atomicAdd(&counters[NSD_CNT_OPS + threadIdx.x], (unsigned long long)sh.ops[threadIdx.x]);
+}
+
 } // namespace nsd
 
 // ---- launcher (C ABI, called by nsd_host.cpp / nsd_pipe.cpp) -----------------
@@ -1056,10 +1541,119 @@ static size_t region_slots(uint32_t n)
 	return ((size_t)n + (size_t)NSD_MAX_GRID * nsd::BLOCK + 1) & ~(size_t)1;
 }
 
-// workspace: the pending-checksum lists (u64 per slot)
+// ---- the schedule -------------------------------------------------------------
+// split (dissect_fast + dissect_walk) or fused (dissect_all).  The split
+// schedule runs the fast walk at 6 waves per SIMD instead of 4 and wins when
+// few packets need the general walk (C2 16M x 64 B: 0.221 against 0.249 ms,
+// C3 equal); when most do (C4's IPv6 extension chains) the fused kernel
+// wins by far (1.17 against 1.88 ms): its walkers take a tile's packets while
+// their first lines are still on chip, where the walker kernel re-reads them
+// and the fast kernel writes a list entry per packet.  Adaptive (the
+// default): every NSD_SCHED_SAMPLE launches on a device the launcher queues a
+// copy of the device's deferral count (g_deferred, the packets the fast walk
+// handed over) to pinned host memory and resets it; once a copy has landed,
+// the share of deferred packets picks the schedule for the launches after
+// it, with hysteresis (fused above 15 %, split again below 5 %).  A capture's
+// traffic mix changes slowly against batches of a few milliseconds; both
+// schedules give identical results.  nsd_set_schedule forces one (tests).
+#ifndef NSD_SCHED_SAMPLE
+#define NSD_SCHED_SAMPLE 16
+#endif
+namespace {
+constexpr int MAX_DEV = 16;
+struct Sched {
+	bool init = false, fused = false, pending = false;
+	int launches = 0;
+	uint64_t pkts = 0, sampled = 0;   // packets since the last sample / in the sample in flight
+	unsigned long long *host = nullptr;
+	void *dev_acc = nullptr;
+	hipEvent_t ev = nullptr;
+};
+Sched g_sched[MAX_DEV];
+std::mutex g_sched_mu;
+int g_sched_force = 0;   // 0 adaptive, NSD_SCHED_SPLIT, NSD_SCHED_FUSED
+int g_sched_last = 0;
+
+int cur_dev()
+{
+	int d = 0;
+	if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAX_DEV)
+		d = 0;
+	return d;
+}
+
+// the schedule of a launch of n packets on the current device
+bool sched_fused(uint32_t n)
+{
+	std::lock_guard<std::mutex> g(g_sched_mu);
+	Sched &S = g_sched[cur_dev()];
+	bool fused;
+	if (g_sched_force) {
+		fused = g_sched_force == NSD_SCHED_FUSED;
+	} else {
+		if (S.pending && hipEventQuery(S.ev) == hipSuccess) {
+			const double rate = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
+			S.fused = S.fused ? rate > 0.05 : rate > 0.15;
+			S.pending = false;
+		}
+		fused = S.fused;
+	}
+	S.pkts += n;
+	S.launches++;
+	g_sched_last = fused ? NSD_SCHED_FUSED : NSD_SCHED_SPLIT;
+	return fused;
+}
+
+// after a launch on `stream`: queue the deferral sample when one is due
+void sched_sample(hipStream_t stream)
+{
+	std::lock_guard<std::mutex> g(g_sched_mu);
+	Sched &S = g_sched[cur_dev()];
+	if (g_sched_force || S.pending || S.launches < NSD_SCHED_SAMPLE)
+		return;
+	if (!S.init) {
+		S.init = true;
+		if (hipHostMalloc((void **)&S.host, 8, hipHostMallocDefault) != hipSuccess ||
+		    hipGetSymbolAddress(&S.dev_acc, HIP_SYMBOL(nsd::g_deferred)) != hipSuccess ||
+		    hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
+			S.host = nullptr;
+	}
+	if (!S.host)
+		return;
+	if (hipMemcpyAsync(S.host, S.dev_acc, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+	    hipMemsetAsync(S.dev_acc, 0, 8, stream) != hipSuccess || hipEventRecord(S.ev, stream) != hipSuccess)
+		return;
+	S.sampled = S.pkts;
+	S.pkts = 0;
+	S.launches = 0;
+	S.pending = true;
+}
+} // namespace
+
+extern "C" int nsd_set_schedule(int sched)
+{
+	if (sched != NSD_SCHED_ADAPTIVE && sched != NSD_SCHED_SPLIT && sched != NSD_SCHED_FUSED)
+		return NSD_ERR_ARG;
+	std::lock_guard<std::mutex> g(g_sched_mu);
+	const int prev = g_sched_force;
+	g_sched_force = sched;
+	return prev;
+}
+
+extern "C" int nsd_last_schedule(void)
+{
+	std::lock_guard<std::mutex> g(g_sched_mu);
+	return g_sched_last;
+}
+
+// workspace: the fused kernel's pending lists (u64 per slot); the split
+// schedule's fast lists (up to 32 bytes per slot), their counts and the
+// walker kernel's pending lists (u64 per slot, up to two per packet slot)
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
-	return 8 * region_slots(n);
+	const size_t slots = region_slots(n);
+	return align256(32 * slots) + align256((size_t)NSD_MAX_GRID * nsd::WAVES * 8) + 16 * slots + 256;
 }
 
 extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
@@ -1094,55 +1688,107 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 				      int grid, hipStream_t stream)
 {
 	using namespace nsd;
-	typedef void (*kfn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, uint32_t *, uint32_t,
-			    uint32_t *, uint32_t, unsigned long long *, uint64_t *, uint32_t, const uint32_t *);
-	static const kfn kernels[2][3] = {
-		{ dissect_all<PRINT_NORM, false>, dissect_all<PRINT_LESS, false>, dissect_all<PRINT_HEX, false> },
-		{ dissect_all<PRINT_NORM, true>, dissect_all<PRINT_LESS, true>, dissect_all<PRINT_HEX, true> },
-	};
-	static int s_cus = 0;
 	if (n == 0)
 		return 0;
+	static int s_cus = 0;
 	if (!s_cus) {
 		int dev = 0;
 		if (hipGetDevice(&dev) != hipSuccess ||
 		    hipDeviceGetAttribute(&s_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
 			s_cus = 256;
 	}
-	const uint32_t waves = (n + 63) / 64;
-	uint32_t blocks = (waves + WAVES - 1) / WAVES;
-	// persistent grid: exactly the blocks that are resident together (CUs x
-	// the kernel's occupancy), so no block waits for a second round; every
-	// block grid-strides (counters then cost one flush per block)
-	static int s_occ[2][3] = { { 0, 0, 0 }, { 0, 0, 0 } };
 	const int mi = mode == PRINT_NORM ? 0 : mode == PRINT_LESS ? 1 : 2;
 	const int ci = compact ? 1 : 0;
-	const kfn f = kernels[ci][mi];
-	if (!s_occ[ci][mi]) {
-		int occ = 0;
-		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)f, BLOCK, 0) != hipSuccess ||
-		    occ < 1)
-			occ = 4;
-		s_occ[ci][mi] = occ;
-	}
-	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)(s_cus * s_occ[ci][mi]);
-	if (cap_blocks > NSD_MAX_GRID)
-		cap_blocks = NSD_MAX_GRID;
-	if (blocks > cap_blocks)
-		blocks = cap_blocks;
-	const uint32_t region = region_for(n, blocks);
-	uint64_t *pend = (uint64_t *)d_ws;
+	const uint32_t waves = (n + 63) / 64;
+	const uint32_t want = (waves + WAVES - 1) / WAVES;
 	// ext pool chunk per request: half the pool spread over the waves, so the
 	// unused chunk tails the waves keep at the end waste at most half of it
 	// (a pool of 2x the words the chains need never overflows), within
 	// [1 deep entry, 512 short entries]
 	if (ext_words > NSD_EXT_POOL_MAX_WORDS)
 		ext_words = NSD_EXT_POOL_MAX_WORDS;
-	const uint64_t per = (uint64_t)ext_words / (2ull * blocks * WAVES);
-	const uint32_t lo = NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS), hi = 512 * NSD_EXT_WORDS(16);
-	const uint32_t chunk = (uint32_t)(per < lo ? lo : per > hi ? hi : per) & ~3u;
+	auto chunk_for = [&](uint32_t blocks) {
+		const uint64_t per = (uint64_t)ext_words / (2ull * blocks * WAVES);
+		const uint32_t lo = NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS), hi = 512 * NSD_EXT_WORDS(16);
+		return (uint32_t)(per < lo ? lo : per > hi ? hi : per) & ~3u;
+	};
+	// persistent grids: exactly the blocks that are resident together (CUs x
+	// the kernel's occupancy), so no block waits for a second round; every
+	// block grid-strides (counters then cost one flush per block)
+	auto occupancy = [&](const void *f, int &slot, int dflt) {
+		if (!slot) {
+			int occ = 0;
+			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, BLOCK, 0) != hipSuccess || occ < 1)
+				occ = dflt;
+			slot = occ;
+		}
+		return slot;
+	};
+	const bool fused = mi != 2 && sched_fused(n);
+	if (fused) {
+	typedef void (*kfn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, uint32_t *, uint32_t,
+			    uint32_t *, uint32_t, unsigned long long *, uint64_t *, uint32_t, const uint32_t *);
+	static const kfn kernels[2][3] = {
+		{ dissect_all<PRINT_NORM, false>, dissect_all<PRINT_LESS, false>, dissect_all<PRINT_HEX, false> },
+		{ dissect_all<PRINT_NORM, true>, dissect_all<PRINT_LESS, true>, dissect_all<PRINT_HEX, true> },
+	};
+	static int s_occ[2][3];
+	const kfn f = kernels[ci][mi];
+	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)(s_cus * occupancy((const void *)f, s_occ[ci][mi], 4));
+	if (cap_blocks > NSD_MAX_GRID)
+		cap_blocks = NSD_MAX_GRID;
+	const uint32_t blocks = want < cap_blocks ? want : cap_blocks;
 	hipLaunchKernelGGL(f, dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec, d_ext,
-			   ext_words, d_ext_used, chunk, (unsigned long long *)d_counters, pend, region,
-			   (const uint32_t *)d_sll);
-	return hipGetLastError() == hipSuccess ? 0 : -2;
+			   ext_words, d_ext_used, chunk_for(blocks), (unsigned long long *)d_counters, (uint64_t *)d_ws,
+			   region_for(n, blocks), (const uint32_t *)d_sll);
+	if (hipGetLastError() != hipSuccess)
+		return -2;
+	sched_sample(stream);
+	return 0;
+	}
+	typedef void (*ffn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, unsigned long long *, uint4 *,
+			    uint32_t, uint2 *, const uint32_t *);
+	typedef void (*wfn)(const uint8_t *, const uint64_t *, uint32_t, void *, uint32_t *, uint32_t, uint32_t *,
+			    uint32_t, unsigned long long *, const uint4 *, uint32_t, const uint2 *, uint32_t, uint64_t *,
+			    uint32_t);
+	static const ffn fast[2][3] = {
+		{ dissect_fast<PRINT_NORM, false>, dissect_fast<PRINT_LESS, false>, dissect_fast<PRINT_HEX, false> },
+		{ dissect_fast<PRINT_NORM, true>, dissect_fast<PRINT_LESS, true>, dissect_fast<PRINT_HEX, true> },
+	};
+	static const wfn walk[2][2] = {
+		{ dissect_walk<PRINT_NORM, false>, dissect_walk<PRINT_LESS, false> },
+		{ dissect_walk<PRINT_NORM, true>, dissect_walk<PRINT_LESS, true> },
+	};
+	static int s_focc[2][3], s_wocc[2][2];
+	// grid > 0 (tests): both kernels' grids capped at `grid` blocks
+	uint32_t fcap = grid > 0 ? (uint32_t)grid
+				 : (uint32_t)(s_cus * occupancy((const void *)fast[ci][mi], s_focc[ci][mi], 8));
+	if (fcap > NSD_MAX_GRID)
+		fcap = NSD_MAX_GRID;
+	const uint32_t fblocks = want < fcap ? want : fcap;
+	const uint32_t cap = region_for(n, fblocks) / WAVES;   // slots per fast wave
+	const uint32_t nlists = fblocks * WAVES;
+	const size_t slotb = 32;   // a list slot: two uint4 (fast_tiles)
+	uint8_t *ws = (uint8_t *)d_ws;
+	uint4 *lists = (uint4 *)ws;
+	uint2 *cnts = (uint2 *)(ws + align256(slotb * nlists * cap));
+	uint64_t *pend = (uint64_t *)((uint8_t *)cnts + align256((size_t)nlists * 8));
+	hipLaunchKernelGGL(fast[ci][mi], dim3(fblocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec,
+			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll);
+	if (hipGetLastError() != hipSuccess)
+		return -2;
+	if (mi == 2)
+		return 0;   // no chains: nothing deferred
+	uint32_t wcap = grid > 0 ? (uint32_t)grid
+				 : (uint32_t)(s_cus * occupancy((const void *)walk[ci][mi], s_wocc[ci][mi], 4));
+	const uint32_t wblocks = fblocks < wcap ? fblocks : wcap;
+	const uint32_t per_wave = (nlists + wblocks * WAVES - 1) / (wblocks * WAVES);   // lists per walker wave
+	hipLaunchKernelGGL(walk[ci][mi], dim3(wblocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, d_rec, d_ext,
+			   ext_words, d_ext_used, chunk_for(wblocks), (unsigned long long *)d_counters, lists, cap, cnts,
+			   nlists, pend, per_wave * cap * WAVES);
+	if (hipGetLastError() != hipSuccess)
+		return -2;
+	sched_sample(stream);
+	return 0;
 }
+

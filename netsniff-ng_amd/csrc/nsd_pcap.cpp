@@ -31,6 +31,11 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <sys/uio.h>
+
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -38,8 +43,10 @@
 #include "../../include/netsniff_dissect.h"
 
 namespace nsd {
-void render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
-		       const nsd_sll_t *sll);
+int render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
+		      const nsd_sll_t *sll);
+int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+			  const nsd_crec &rec, uint32_t i, const uint32_t *ext_pool, const nsd_sll_t *sll);
 void cpu_count_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode, const nsd_sll_t *sll,
 		      uint64_t *counters);
 }
@@ -357,6 +364,19 @@ static bool push_fhdr(const nsd_pcap *p, int fd)
 // every record that passed the filter exactly as it was read (record header
 // incl. the *_LL cooked header, then its bytes: write_pcap(fdo, &phdr, magic,
 // out, pcap_get_length) of pcap_sg.c / pcap_rw.c), in file order.
+//
+// Three stages run at once over a ring of batch slots (pinned host buffers):
+//   - this thread reads a batch, filters it and submits it to the device
+//     pipe (compact records, DEPTH batches in flight); when the pipe is full
+//     it completes the oldest batch and queues its render jobs;
+//   - `threads` formatter threads (a pool for the whole replay) render the
+//     batch's contiguous packet ranges, each into its own text buffer;
+//   - a writer thread writes each batch's buffers in file order (writev, or
+//     through the tprintf wrap when cols > 0), then the pcap write-out, and
+//     frees the slot.
+// So reading and walking batch k+1 overlap the rendering of batch k and the
+// writing of batch k-1.  A record above NSD_MAX_CAPLEN waits for everything
+// before it to be written, then goes through the per-packet path.
 extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_prog *filter, int out_fd,
 				    int cols, uint64_t *counters, int threads, int pcap_fd)
 {
@@ -367,182 +387,244 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	if (threads > 64)
 		threads = 64;
 	constexpr uint32_t BATCH = 1u << 16;
-	constexpr size_t FRAME_BYTES = 64ull << 20;
-	constexpr int DEPTH = 3;
+	constexpr size_t FRAME_BYTES = 32ull << 20;
+	constexpr int DEPTH = 3;           // batches on the device
+	constexpr int NSLOT = DEPTH + 3;   // + being rendered, rendered, being written
 	nsd_pcap *p = nsd_pcap_open(path);
 	if (!p)
 		return NSD_ERR_ARG;
 	const int lt = (int)p->linktype;
 	const bool has_ll = p->ll_extra != 0;   // *_LL file: one sockaddr_ll per record
-	// room for every record of the batch to take a deep (> 16 layer) entry;
-	// a chain the pool still cannot hold is re-rendered on the host (below)
-	const uint32_t ext_words = 2u * NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS) * BATCH;
+	// the side words and room for a quarter of the batch to take a deep (> 12
+	// layer) entry; a chain the pool cannot hold is rendered per packet (below)
+	const uint32_t ext_words = BATCH + BATCH / 4 * NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS);
 	if (pcap_fd >= 0 && !push_fhdr(p, pcap_fd)) {
 		nsd_pcap_close(p);
 		return NSD_ERR_ARG;
 	}
-	nsd_pipe *pipe = nsd_pipe_create(BATCH, FRAME_BYTES, ext_words, DEPTH, lt, mode);
+	nsd_pipe *pipe = nsd_pipe_create_compact(BATCH, FRAME_BYTES, ext_words, DEPTH, lt, mode);
 	if (!pipe) {
 		nsd_pcap_close(p);
 		return NSD_ERR_HIP;
 	}
-	struct Batch {
+	struct Slot {
 		uint8_t *frames = nullptr;
 		nsd_desc_t *desc = nullptr;
 		nsd_sll_t *sll = nullptr;
 		uint8_t *rhdr = nullptr;   // record headers as read (pcap write-out)
-		nsd_rec *rec = nullptr;
+		nsd_crec *rec = nullptr;
 		uint32_t *ext = nullptr;
 		uint32_t *verdict = nullptr;
 		uint32_t ext_used = 0, n = 0;
 		uint64_t cnt[NSD_NCOUNTERS];
 		int status = 0;
-		bool busy = false;
+		uint64_t seq = 0;
+		int parts = 0, left = 0;   // render jobs, jobs not done
+		std::vector<std::string> part;
+		long prc = NSD_OK;         // first render error
 	};
-	Batch b[DEPTH];
-	long rc = 0, printed = 0;
-	long wrap_state = 0;
-	std::string text, wrapped;
+	std::vector<Slot> b(NSLOT);
+	long rc = NSD_OK;
 	for (auto &x : b) {
 		x.frames = (uint8_t *)nsd_host_alloc(FRAME_BYTES);
 		x.desc = (nsd_desc_t *)nsd_host_alloc(BATCH * sizeof(nsd_desc_t));
-		x.rec = (nsd_rec *)nsd_host_alloc(BATCH * sizeof(nsd_rec));
+		x.rec = (nsd_crec *)nsd_host_alloc(BATCH * sizeof(nsd_crec));
 		x.ext = (uint32_t *)nsd_host_alloc(ext_words * sizeof(uint32_t));
 		x.verdict = (uint32_t *)malloc(BATCH * sizeof(uint32_t));
 		if (has_ll)
 			x.sll = (nsd_sll_t *)nsd_host_alloc(BATCH * sizeof(nsd_sll_t));
 		if (pcap_fd >= 0)
 			x.rhdr = (uint8_t *)malloc((size_t)BATCH * 32);
+		x.part.resize(threads);
 		if (!x.frames || !x.desc || !x.rec || !x.ext || !x.verdict || (has_ll && !x.sll) ||
 		    (pcap_fd >= 0 && !x.rhdr))
 			rc = NSD_ERR_NOMEM;
 	}
-	// text out (tprintf-wrapped at `cols` > 0), then the records to the pcap
-	// write-out, for `n` records whose text is in `text`
-	auto emit = [&](uint32_t n, const std::string &recs) -> long {
-		const char *w = text.data();
-		size_t wn = text.size();
-		if (cols > 0 && wn) {
-			wrapped.resize(2 * wn + 16);
-			long k = nsd_tprintf_wrap(text.data(), wn, cols, &wrap_state, &wrapped[0], wrapped.size());
+
+	std::mutex mu;
+	std::condition_variable cv_job, cv_write, cv_free;
+	std::deque<std::pair<int, int>> jobs;   // (slot, part)
+	std::vector<int> free_slots;
+	for (int k = NSLOT - 1; k >= 0; k--)
+		free_slots.push_back(k);
+	std::deque<int> to_write;               // slots in file order, waiting for their render
+	uint64_t next_seq = 0, written = 0;     // batches handed to the writer / written
+	long err = rc;                          // first error of any stage
+	bool stop = false;
+	long printed = 0;
+	long wrap_state = 0;
+	std::string wrapped;
+
+	// the writer's output of one piece of text (wrapped when cols > 0)
+	auto put_text = [&](const std::string &t) -> long {
+		if (cols > 0 && !t.empty()) {
+			wrapped.resize(2 * t.size() + 16);
+			const long k = nsd_tprintf_wrap(t.data(), t.size(), cols, &wrap_state, &wrapped[0], wrapped.size());
 			if (k < 0)
 				return k;
-			w = wrapped.data();
-			wn = (size_t)k;
+			return write_all(out_fd, wrapped.data(), (size_t)k) ? NSD_OK : NSD_ERR_ARG;
 		}
-		if (!write_all(out_fd, w, wn))
-			return NSD_ERR_ARG;
-		if (pcap_fd >= 0 && !write_all(pcap_fd, recs.data(), recs.size()))
-			return NSD_ERR_ARG;
-		printed += n;
+		return write_all(out_fd, t.data(), t.size()) ? NSD_OK : NSD_ERR_ARG;
+	};
+	auto put_parts = [&](const Slot &x) -> long {
+		if (cols > 0) {
+			for (int t = 0; t < x.parts; t++) {
+				const long r = put_text(x.part[t]);
+				if (r != NSD_OK)
+					return r;
+			}
+			return NSD_OK;
+		}
+		std::vector<struct iovec> iov;
+		for (int t = 0; t < x.parts; t++)
+			if (!x.part[t].empty())
+				iov.push_back({ (void *)x.part[t].data(), x.part[t].size() });
+		size_t k = 0;
+		while (k < iov.size()) {
+			const int cnt = (int)(iov.size() - k < 512 ? iov.size() - k : 512);
+			ssize_t w = writev(out_fd, &iov[k], cnt);
+			if (w < 0 && errno == EINTR)
+				continue;
+			if (w <= 0)
+				return NSD_ERR_ARG;
+			while (w > 0 && k < iov.size()) {   // advance past what was written
+				if ((size_t)w >= iov[k].iov_len) {
+					w -= (ssize_t)iov[k].iov_len;
+					k++;
+				} else {
+					iov[k].iov_base = (uint8_t *)iov[k].iov_base + w;
+					iov[k].iov_len -= (size_t)w;
+					w = 0;
+				}
+			}
+		}
 		return NSD_OK;
 	};
-	// complete the oldest batch and print it
-	auto finish = [&](Batch &x) -> long {
-		int st = nsd_pipe_wait(pipe);
-		x.busy = false;
-		if (st != NSD_OK)
-			return st < 0 ? st : NSD_ERR_HIP;
-		if (x.status != NSD_OK)
-			return x.status;
-		if (counters)
-			for (int k = 0; k < NSD_NCOUNTERS; k++)
-				counters[k] += x.cnt[k];
-		// render the batch on `threads` host threads over contiguous packet
-		// ranges (records are independent; only the wrap carries state), then
-		// join the pieces in order
-		const uint32_t nt = x.n < 2048 ? 1u : (uint32_t)threads;
-		std::vector<std::string> part(nt);
-		std::vector<long> prc(nt, NSD_OK);
-		auto render = [&](uint32_t t) {
-			const uint32_t lo = (uint32_t)((uint64_t)x.n * t / nt), hi = (uint32_t)((uint64_t)x.n * (t + 1) / nt);
-			size_t cap = 256 * (size_t)(hi - lo) + 4096;
-			std::vector<uint64_t> ends(hi - lo);
-			std::vector<int8_t> st(hi - lo);
-			for (;;) {
-				part[t].resize(cap);
-				long r = nsd_format_batch_sll(x.frames, x.desc + lo, x.sll ? x.sll + lo : nullptr,
-							      hi - lo, lt, mode, x.rec + lo, x.ext, &part[t][0],
-							      cap, ends.data(), st.data());
-				if (r >= 0) {
-					part[t].resize((size_t)r);
-					break;
-				}
-				cap = (size_t)(-r);
-			}
-			// a record that could not hold its chain (NSD_F_OVERFLOW: longer
-			// than NSD_EXT_MAX_LAYERS layers, or the ext pool was exhausted)
-			// is rendered by the per-packet path, which has no layer budget;
-			// any other status is an error
-			bool redo = false;
-			for (uint32_t k = lo; k < hi; k++) {
-				if (!st[k - lo])
-					continue;
-				if (!(x.rec[k].nflags & NSD_F_OVERFLOW)) {
-					prc[t] = NSD_ERR_FORMAT;
-					return;
-				}
-				redo = true;
-			}
-			if (!redo)
-				return;
-			std::string fixed;
-			size_t prev = 0;
-			for (uint32_t k = lo; k < hi; k++) {
-				const size_t e = (size_t)ends[k - lo];
-				if (st[k - lo])
-					nsd::render_packet_cpu(fixed, x.frames + NSD_DESC_OFF(x.desc[k]),
-							       NSD_DESC_CAPLEN(x.desc[k]), lt, mode,
-							       x.sll ? x.sll + k : nullptr);
-				else
-					fixed.append(part[t], prev, e - prev);
-				prev = e;
-			}
-			part[t].swap(fixed);
-		};
-		if (nt == 1) {
-			render(0);
-		} else {
-			std::vector<std::thread> th;
-			for (uint32_t t = 1; t < nt; t++)
-				th.emplace_back(render, t);
-			render(0);
-			for (auto &h : th)
-				h.join();
-		}
-		for (long r : prc)
-			if (r != NSD_OK)
-				return r;
-		text.clear();
-		for (auto &q : part)
-			text += q;
+	auto put_records = [&](const Slot &x) -> long {
+		if (pcap_fd < 0)
+			return NSD_OK;
 		std::string recs;
-		if (pcap_fd >= 0)
-			for (uint32_t k = 0; k < x.n; k++) {
-				recs.append((const char *)x.rhdr + 32 * (size_t)k, p->hdrsize);
-				recs.append((const char *)x.frames + NSD_DESC_OFF(x.desc[k]), NSD_DESC_CAPLEN(x.desc[k]));
-			}
-		return emit(x.n, recs);
-	};
-	// complete every batch in flight, in submission order
-	int slot = 0;
-	auto drain = [&]() -> long {
-		long r0 = NSD_OK;
-		for (int k = 0; k < DEPTH; k++) {
-			Batch &x = b[(slot + k) % DEPTH];
-			if (x.busy) {
-				long r = finish(x);
-				if (r0 == NSD_OK)
-					r0 = r;
-			}
+		for (uint32_t k = 0; k < x.n; k++) {
+			recs.append((const char *)x.rhdr + 32 * (size_t)k, p->hdrsize);
+			recs.append((const char *)x.frames + NSD_DESC_OFF(x.desc[k]), NSD_DESC_CAPLEN(x.desc[k]));
 		}
-		return r0;
+		return write_all(pcap_fd, recs.data(), recs.size()) ? NSD_OK : NSD_ERR_ARG;
+	};
+
+	// formatter pool: part t of a slot = its packets [n t / parts, n (t+1) / parts)
+	auto render = [&](Slot &x, int t) -> long {
+		const uint32_t lo = (uint32_t)((uint64_t)x.n * t / x.parts), hi = (uint32_t)((uint64_t)x.n * (t + 1) / x.parts);
+		std::string &s = x.part[t];
+		s.clear();
+		for (uint32_t k = lo; k < hi; k++) {
+			const uint64_t d = x.desc[k];
+			const size_t mark = s.size();
+			const int r = nsd::format_packet_compact(s, x.frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), lt, mode,
+								 x.rec[k], k, x.ext, x.sll ? x.sll + k : nullptr);
+			if (r == NSD_OK)
+				continue;
+			// a record that could not hold its chain (NSD_F_OVERFLOW: longer
+			// than NSD_EXT_MAX_LAYERS layers, or the ext pool was full) is
+			// rendered by the per-packet path, which has no layer budget;
+			// any other status is an error
+			if (!(x.rec[k].nflags & NSD_F_OVERFLOW))
+				return NSD_ERR_FORMAT;
+			s.resize(mark);
+			const int r2 = nsd::render_packet_cpu(s, x.frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), lt, mode,
+							      x.sll ? x.sll + k : nullptr);
+			if (r2 != NSD_OK)
+				return r2;
+		}
+		return NSD_OK;
+	};
+	std::vector<std::thread> pool;
+	for (int t = 0; t < threads; t++)
+		pool.emplace_back([&]() {
+			std::unique_lock<std::mutex> lk(mu);
+			for (;;) {
+				cv_job.wait(lk, [&] { return stop || !jobs.empty(); });
+				if (jobs.empty())
+					return;
+				const auto j = jobs.front();
+				jobs.pop_front();
+				lk.unlock();
+				const long r = render(b[j.first], j.second);
+				lk.lock();
+				Slot &x = b[j.first];
+				if (r != NSD_OK && x.prc == NSD_OK)
+					x.prc = r;
+				if (--x.left == 0)
+					cv_write.notify_all();
+			}
+		});
+	std::thread writer([&]() {
+		std::unique_lock<std::mutex> lk(mu);
+		for (;;) {
+			cv_write.wait(lk, [&] { return (!to_write.empty() && b[to_write.front()].left == 0) ||
+						       (stop && to_write.empty()); });
+			if (to_write.empty())
+				return;
+			const int k = to_write.front();
+			to_write.pop_front();
+			Slot &x = b[k];
+			long r = x.prc;
+			const bool skip = err != NSD_OK;
+			lk.unlock();
+			if (!skip && r == NSD_OK)
+				r = put_parts(x);
+			if (!skip && r == NSD_OK)
+				r = put_records(x);
+			lk.lock();
+			if (r != NSD_OK && err == NSD_OK)
+				err = r;
+			if (!skip && r == NSD_OK)
+				printed += x.n;
+			written++;
+			free_slots.push_back(k);
+			cv_free.notify_all();
+		}
+	});
+
+	// the device batch in slot k completed: queue its render jobs
+	std::deque<int> on_device;
+	auto complete_oldest = [&]() -> long {
+		const int k = on_device.front();
+		on_device.pop_front();
+		Slot &x = b[k];
+		const int st = nsd_pipe_wait(pipe);
+		long r = st != NSD_OK ? (st < 0 ? st : NSD_ERR_HIP) : x.status;
+		if (r == NSD_OK && counters)
+			for (int c = 0; c < NSD_NCOUNTERS; c++)
+				counters[c] += x.cnt[c];
+		std::lock_guard<std::mutex> g(mu);
+		x.parts = x.n < 2048 ? 1 : threads;
+		x.left = x.parts;
+		x.prc = r;
+		x.seq = next_seq++;
+		to_write.push_back(k);
+		if (r == NSD_OK) {
+			for (int t = 0; t < x.parts; t++)
+				jobs.emplace_back(k, t);
+			cv_job.notify_all();
+		} else {
+			x.left = 0;
+			cv_write.notify_all();
+		}
+		return r;
+	};
+	// everything read so far through the device, rendered and written
+	auto flush_all = [&]() -> long {
+		while (!on_device.empty())
+			complete_oldest();
+		std::unique_lock<std::mutex> lk(mu);
+		cv_free.wait(lk, [&] { return written == next_seq; });
+		return err;
 	};
 	// a record longer than a batch can carry: after the batches before it,
 	// filtered and dissected on its own through the per-packet path
 	std::vector<uint8_t> big;
 	auto one_big = [&]() -> long {
-		long r = drain();
+		long r = flush_all();
 		if (r != NSD_OK)
 			return r;
 		nsd_sll_t ll;
@@ -561,71 +643,113 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		}
 		if (counters)
 			nsd::cpu_count_packet(big.data(), (uint32_t)caplen, lt, mode, has_ll ? &ll : nullptr, counters);
-		text.clear();
-		nsd::render_packet_cpu(text, big.data(), (size_t)caplen, lt, mode, has_ll ? &ll : nullptr);
-		std::string recs;
-		if (pcap_fd >= 0) {
-			recs.append((const char *)hdr, p->hdrsize);
-			recs.append((const char *)big.data(), (size_t)caplen);
-		}
-		return emit(1, recs);
+		std::string text;
+		r = nsd::render_packet_cpu(text, big.data(), (size_t)caplen, lt, mode, has_ll ? &ll : nullptr);
+		if (r != NSD_OK)
+			return r;
+		// (the writer is idle: every batch before this record is written)
+		r = put_text(text);
+		if (r == NSD_OK && pcap_fd >= 0 &&
+		    !(write_all(pcap_fd, hdr, p->hdrsize) && write_all(pcap_fd, big.data(), (size_t)caplen)))
+			r = NSD_ERR_ARG;
+		if (r == NSD_OK)
+			printed++;
+		return r;
 	};
+
 	while (rc == NSD_OK) {
-		Batch &x = b[slot];
-		if (x.busy && (rc = finish(x)) != NSD_OK)
-			break;
+		int k;
+		{
+			std::unique_lock<std::mutex> lk(mu);
+			if (err != NSD_OK) {
+				rc = err;
+				break;
+			}
+			if (free_slots.empty()) {
+				lk.unlock();
+				if (!on_device.empty()) {
+					complete_oldest();
+					continue;
+				}
+				lk.lock();
+				cv_free.wait(lk, [&] { return !free_slots.empty(); });
+			}
+			k = free_slots.back();
+			free_slots.pop_back();
+		}
+		Slot &x = b[k];
+		auto give_back = [&]() {
+			std::lock_guard<std::mutex> g(mu);
+			free_slots.push_back(k);
+		};
 		long n = read_batch(p, x.frames, FRAME_BYTES, x.desc, x.sll, BATCH, nullptr, nullptr, x.rhdr);
 		if (n == NSD_ERR_CAPLEN) {
+			give_back();
 			rc = one_big();
 			continue;
 		}
-		if (n < 0) {
-			rc = n;
+		if (n <= 0) {
+			give_back();
+			if (n < 0)
+				rc = n;
 			break;
 		}
-		if (n == 0)
-			break;
 		size_t used = 0;
-		for (long k = 0; k < n; k++) {
-			const size_t e = NSD_DESC_OFF(x.desc[k]) + NSD_DESC_CAPLEN(x.desc[k]);
+		for (long j = 0; j < n; j++) {
+			const size_t e = NSD_DESC_OFF(x.desc[j]) + NSD_DESC_CAPLEN(x.desc[j]);
 			used = e > used ? e : used;
 		}
 		if (filter) {
 			// bpf_run_filter per record before the dissector (netsniff-ng.c:723-725)
 			int r = nsd_bpf_filter_batch(filter, x.frames, used, x.desc, (uint32_t)n, x.verdict);
 			if (r != NSD_OK) {
+				give_back();
 				rc = r;
 				break;
 			}
 			long m = 0;
-			for (long k = 0; k < n; k++)
-				if (x.verdict[k]) {
+			for (long j = 0; j < n; j++)
+				if (x.verdict[j]) {
 					if (x.sll)
-						x.sll[m] = x.sll[k];
-					if (x.rhdr && m != k)
-						memcpy(x.rhdr + 32 * (size_t)m, x.rhdr + 32 * (size_t)k, 32);
-					x.desc[m++] = x.desc[k];
+						x.sll[m] = x.sll[j];
+					if (x.rhdr && m != j)
+						memcpy(x.rhdr + 32 * (size_t)m, x.rhdr + 32 * (size_t)j, 32);
+					x.desc[m++] = x.desc[j];
 				}
 			n = m;
-			if (n == 0)
+			if (n == 0) {
+				give_back();
 				continue;
+			}
 		}
+		if ((int)on_device.size() == DEPTH)
+			complete_oldest();
 		x.n = (uint32_t)n;
+		x.status = NSD_OK;
 		memset(x.cnt, 0, sizeof(x.cnt));
-		int r = nsd_pipe_submit_sll(pipe, x.frames, used, x.desc, x.sll, x.n, x.rec, x.ext, &x.ext_used,
-					    x.cnt, &x.status);
+		int r = nsd_pipe_submit_compact(pipe, x.frames, used, x.desc, x.sll, x.n, x.rec, x.ext, &x.ext_used, x.cnt,
+						&x.status);
 		if (r != NSD_OK) {
+			give_back();
 			rc = r;
 			break;
 		}
-		x.busy = true;
-		slot = (slot + 1) % DEPTH;
+		on_device.push_back(k);
 	}
 	{
-		const long r = drain();
+		const long r = flush_all();
 		if (rc == NSD_OK)
 			rc = r;
 	}
+	{
+		std::lock_guard<std::mutex> g(mu);
+		stop = true;
+	}
+	cv_job.notify_all();
+	cv_write.notify_all();
+	for (auto &t : pool)
+		t.join();
+	writer.join();
 	for (auto &x : b) {
 		nsd_host_free(x.frames);
 		nsd_host_free(x.desc);

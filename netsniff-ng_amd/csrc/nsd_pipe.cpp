@@ -11,10 +11,10 @@
 
 #include "../../include/netsniff_dissect.h"
 
-extern "C" int nsd_launch_dissect_sll(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
-				      uint32_t n, int start_id, int mode, nsd_rec *d_rec, uint32_t *d_ext,
-				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters,
-				      void *d_ws, int grid, hipStream_t stream);
+extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
+				      uint32_t n, int start_id, int mode, void *d_rec, int compact, uint32_t *d_ext,
+				      uint32_t ext_words, uint32_t *d_ext_used, uint64_t *d_counters, void *d_ws,
+				      int grid, hipStream_t stream);
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n);
 int nsd_start_for(int linktype);
 
@@ -45,6 +45,7 @@ struct Slot {
 	bool busy = false;
 	int status = NSD_OK;
 	uint32_t n = 0;
+	void *rec_out = nullptr;
 	uint32_t *ext_out = nullptr;
 	uint32_t *ext_count_out = nullptr;
 	uint64_t *counters_out = nullptr;
@@ -59,6 +60,7 @@ struct nsd_pipe {
 	int depth = 0;
 	int start_id = 0;
 	int mode = 0;
+	bool compact = false;   // nsd_crec records (nsd_pipe_create_compact)
 	int head = 0;    // oldest in flight
 	int count = 0;   // in flight
 	Slot slot[MAX_DEPTH];
@@ -89,8 +91,23 @@ extern "C" void nsd_pipe_destroy(nsd_pipe *p)
 	delete p;
 }
 
+static nsd_pipe *pipe_create(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_cap, int depth, int linktype,
+			     int mode, bool compact);
+
 extern "C" nsd_pipe *nsd_pipe_create(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_cap,
 				     int depth, int linktype, int mode)
+{
+	return pipe_create(max_pkts, max_frame_bytes, ext_cap, depth, linktype, mode, false);
+}
+
+extern "C" nsd_pipe *nsd_pipe_create_compact(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_cap,
+					     int depth, int linktype, int mode)
+{
+	return pipe_create(max_pkts, max_frame_bytes, ext_cap, depth, linktype, mode, true);
+}
+
+static nsd_pipe *pipe_create(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_cap, int depth, int linktype,
+			     int mode, bool compact)
 {
 	if (!max_pkts || !max_frame_bytes || depth < 1 || depth > MAX_DEPTH || mode < PRINT_NORM ||
 	    mode > PRINT_NONE)
@@ -105,6 +122,7 @@ extern "C" nsd_pipe *nsd_pipe_create(uint32_t max_pkts, size_t max_frame_bytes, 
 	p->depth = depth;
 	p->start_id = nsd_start_for(linktype);
 	p->mode = mode;
+	p->compact = compact;
 	for (int k = 0; k < depth; k++) {
 		Slot &s = p->slot[k];
 		bool good = ok(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "stream") &&
@@ -138,7 +156,10 @@ static int complete_oldest(nsd_pipe *p)
 			memcpy(s.counters_out, s.small_h + 8, NSD_NCOUNTERS * 8);
 		if (s.ext_count_out)
 			*s.ext_count_out = used;
-		const uint32_t k = used < p->ext_cap ? used : p->ext_cap;
+		// compact records: the side words [0, n) and the entries after them,
+		// only when a record of the batch needs either
+		const uint64_t need = p->compact ? (s.small_h[8 + NSD_CNT_EXT] ? (uint64_t)s.n + used : 0) : used;
+		const uint32_t k = need < p->ext_cap ? (uint32_t)need : p->ext_cap;
 		if (k && s.ext_out &&
 		    !ok(hipMemcpyAsync(s.ext_out, s.ext, (size_t)k * 4, hipMemcpyDeviceToHost,
 				       s.stream), "ext D2H"))
@@ -187,9 +208,31 @@ extern "C" int nsd_pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames
 // same, with one sockaddr_ll per packet (pkt->sll of the SLL heads; the
 // *_LL pcap record's cooked header or the RX ring's per-frame sockaddr_ll);
 // sll may be NULL (the heads read zeros)
+static int pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len, const nsd_desc_t *desc,
+		       const nsd_sll_t *sll, uint32_t n, void *rec, uint32_t *ext, uint32_t *ext_count,
+		       uint64_t *counters, int *status);
+
 extern "C" int nsd_pipe_submit_sll(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
 				   const nsd_desc_t *desc, const nsd_sll_t *sll, uint32_t n, nsd_rec *rec,
 				   uint32_t *ext, uint32_t *ext_count, uint64_t *counters, int *status)
+{
+	if (p && p->compact)
+		return NSD_ERR_ARG;
+	return pipe_submit(p, frames, frames_len, desc, sll, n, rec, ext, ext_count, counters, status);
+}
+
+extern "C" int nsd_pipe_submit_compact(nsd_pipe *p, const uint8_t *frames, size_t frames_len,
+				       const nsd_desc_t *desc, const nsd_sll_t *sll, uint32_t n, nsd_crec *crec,
+				       uint32_t *ext, uint32_t *ext_count, uint64_t *counters, int *status)
+{
+	if (p && !p->compact)
+		return NSD_ERR_ARG;
+	return pipe_submit(p, frames, frames_len, desc, sll, n, crec, ext, ext_count, counters, status);
+}
+
+static int pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len, const nsd_desc_t *desc,
+		       const nsd_sll_t *sll, uint32_t n, void *rec, uint32_t *ext, uint32_t *ext_count,
+		       uint64_t *counters, int *status)
 {
 	if (!p || (n && (!frames || !desc || !rec)) || (p->ext_cap && !ext && n))
 		return NSD_ERR_ARG;
@@ -208,6 +251,7 @@ extern "C" int nsd_pipe_submit_sll(nsd_pipe *p, const uint8_t *frames, size_t fr
 	Slot &s = p->slot[k];
 	s.busy = true;
 	s.n = n;
+	s.rec_out = rec;
 	s.ext_out = ext;
 	s.ext_count_out = ext_count;
 	s.counters_out = counters;
@@ -215,6 +259,7 @@ extern "C" int nsd_pipe_submit_sll(nsd_pipe *p, const uint8_t *frames, size_t fr
 	s.status = NSD_OK;
 	p->count++;
 	const hipStream_t st = s.stream;
+	const size_t rb = p->compact ? sizeof(nsd_crec) : sizeof(nsd_rec);
 	bool good = ok(hipMemsetAsync(s.small, 0, 64 + NSD_NCOUNTERS * 8, st), "memset");
 	if (good && n) {
 		good = ok(hipMemcpyAsync(s.frames, frames, frames_len, hipMemcpyHostToDevice, st), "H2D") &&
@@ -222,12 +267,11 @@ extern "C" int nsd_pipe_submit_sll(nsd_pipe *p, const uint8_t *frames, size_t fr
 		       ok(hipMemcpyAsync(s.desc, desc, (size_t)n * 8, hipMemcpyHostToDevice, st), "H2D") &&
 		       (!sll || ok(hipMemcpyAsync(s.sll, sll, (size_t)n * sizeof(nsd_sll_t), hipMemcpyHostToDevice,
 						  st), "H2D"));
-		good = good && nsd_launch_dissect_sll(s.frames, s.desc, sll ? s.sll : nullptr, n, p->start_id,
-						      p->mode, s.rec, p->ext_cap ? s.ext : nullptr, p->ext_cap,
-						      s.small, (uint64_t *)((uint8_t *)s.small + 64), s.ws, 0,
+		good = good && nsd_launch_dissect_rec(s.frames, s.desc, sll ? s.sll : nullptr, n, p->start_id,
+						      p->mode, s.rec, p->compact ? 1 : 0, p->ext_cap ? s.ext : nullptr,
+						      p->ext_cap, s.small, (uint64_t *)((uint8_t *)s.small + 64), s.ws, 0,
 						      st) == 0;
-		good = good && ok(hipMemcpyAsync(rec, s.rec, (size_t)n * sizeof(nsd_rec), hipMemcpyDeviceToHost,
-						 st), "D2H");
+		good = good && ok(hipMemcpyAsync(rec, s.rec, (size_t)n * rb, hipMemcpyDeviceToHost, st), "D2H");
 	}
 	good = good && ok(hipMemcpyAsync(s.small_h, s.small, 64 + NSD_NCOUNTERS * 8, hipMemcpyDeviceToHost,
 					 st), "D2H") &&

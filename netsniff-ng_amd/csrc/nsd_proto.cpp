@@ -44,8 +44,8 @@ void render_hex(std::string &s, const uint8_t *pkt, uint32_t caplen, uint32_t fr
 void render_ascii(std::string &s, const uint8_t *pkt, uint32_t caplen, uint32_t from, uint32_t len);
 int cpu_step(int mode, const uint8_t *pkt, uint32_t caplen, int id, uint32_t &data, uint32_t &tail,
 	     uint16_t &ip_csum, uint8_t &flags, const nsd_sll_t *sll);
-void render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
-		       const nsd_sll_t *sll);
+int render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
+		      const nsd_sll_t *sll);
 }
 
 extern "C" __attribute__((visibility("hidden"))) void nsd_device_ctx_release(void);
@@ -207,8 +207,10 @@ extern "C" void hex_ascii(struct pkt_buff *pkt) { hex_ascii_impl(pkt); }
 namespace {
 struct protocol *ops_of(int id);
 
-// ops `id`'s process() in `mode`: one layer at the pkt_buff cursor
-void run_layer(struct pkt_buff *pkt, int id, int mode)
+// ops `id`'s process() in `mode`: one layer at the pkt_buff cursor.  A walk
+// and renderer that disagree are a bug: process() aborts (the reference's
+// bug_on), render_packet_cpu (strict false) gets false back and reports it
+bool run_layer(struct pkt_buff *pkt, int id, int mode, bool strict = true)
 {
 	const uint8_t *head = pkt->head;
 	const uint32_t caplen = t_frame.head == head ? t_frame.caplen : (uint32_t)(pkt->tail - head);
@@ -227,9 +229,14 @@ void run_layer(struct pkt_buff *pkt, int id, int mode)
 	uint32_t rdata, rtail;
 	bool rnext;
 	if (!nsd::render_layer(s, head, caplen, id, start, tail, mode, csum, flags & NSD_F_ICMP_BAD, sll, rdata,
-			       rtail, rnext))
+			       rtail, rnext)) {
+		if (!strict)
+			return false;
 		bug("layer cannot be rendered", id);
+	}
 	if (rdata != data || rtail != ntail || rnext != (next != 0)) {
+		if (!strict)
+			return false;
 		bug("walk and renderer disagree on the layer's end", id);
 	}
 	out(s);
@@ -237,6 +244,7 @@ void run_layer(struct pkt_buff *pkt, int id, int mode)
 	pkt->tail = pkt->head + ntail;
 	if (next)
 		pkt->dissector = ops_of(next);   // pkt_set_dissector (pkt_buff.h:102-110)
+	return true;
 }
 
 template <int ID>
@@ -459,13 +467,18 @@ extern "C" void dissector_entry_point(uint8_t *packet, size_t len, int linktype,
 // mode, ...), as read_pcap calls them), appended to out instead of going to
 // tprintf.  The pcap replay uses it for the records a batch cannot carry: a
 // frame above NSD_MAX_CAPLEN, or a chain the record and its ext pool could
-// not hold (NSD_F_OVERFLOW).  The reference objects' 802.11 / netlink ops
-// run with whatever print type their initialiser gave them.
-void nsd::render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
-			    const nsd_sll_t *sll)
+// not hold (NSD_F_OVERFLOW).  It depends on no global print type: this
+// library's ops run their layer in `mode`, none_ops as the start op (an
+// unknown link type, dissector.c:100-103) prints what its process() would in
+// `mode` (hex_ascii / none_less, proto_none.c:61-83).  The reference's own
+// 802.11 / netlink objects print through tprintf, outside this text: a chain
+// that reaches one returns NSD_ERR_UNSUPPORTED, and a walk / renderer
+// disagreement NSD_ERR_FORMAT (the text so far stays in `text`).
+int nsd::render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
+			   const nsd_sll_t *sll)
 {
 	if (mode == PRINT_NONE)
-		return;
+		return NSD_OK;
 	struct sockaddr_ll *ll = (struct sockaddr_ll *)sll;
 	struct pkt_buff pkt;
 	pkt.head = (uint8_t *)packet;
@@ -479,6 +492,7 @@ void nsd::render_packet_cpu(std::string &text, const uint8_t *packet, size_t len
 	t_frame.head = packet;
 	t_frame.caplen = (uint32_t)len;
 	t_capture = &text;
+	int rc = NSD_OK;
 	struct protocol *start, *end;
 	start_end(linktype, start, end);
 	if (mode == PRINT_NORM || mode == PRINT_LESS) {
@@ -486,21 +500,29 @@ void nsd::render_packet_cpu(std::string &text, const uint8_t *packet, size_t len
 			struct protocol *d = pkt.dissector;
 			pkt.dissector = nullptr;
 			const int id = id_of(d);
-			if (id)
-				run_layer(&pkt, id, mode);
-			else if (d->process)
-				d->process(&pkt);
-			else
+			if (id) {
+				if (!run_layer(&pkt, id, mode, false)) {
+					rc = NSD_ERR_FORMAT;
+					break;
+				}
+			} else if (d == &none_ops) {
+				(mode == PRINT_NORM ? hex_ascii_impl : none_less)(&pkt);
+			} else {
+				rc = NSD_ERR_UNSUPPORTED;
 				break;
+			}
 		}
-		if (end == &none_ops)
+		if (rc == NSD_OK && end == &none_ops)
 			(mode == PRINT_NORM ? hex_ascii_impl : none_less)(&pkt);
 	}
-	switch (mode) {
-	case PRINT_HEX: hex_impl(&pkt); break;
-	case PRINT_ASCII: ascii_impl(&pkt); break;
-	case PRINT_HEX_ASCII: hex_ascii_impl(&pkt); break;
+	if (rc == NSD_OK) {
+		switch (mode) {
+		case PRINT_HEX: hex_impl(&pkt); break;
+		case PRINT_ASCII: ascii_impl(&pkt); break;
+		case PRINT_HEX_ASCII: hex_ascii_impl(&pkt); break;
+		}
 	}
 	t_capture = saved_cap;
 	t_frame = saved;
+	return rc;
 }

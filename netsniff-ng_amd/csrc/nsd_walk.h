@@ -81,6 +81,7 @@ struct WalkOut {
 	int      id;         // next ops to run (0 = chain ended)
 	bool     icmp_pend;  // ICMPv4 checksum left to the wave-cooperative pass
 	uint32_t icmp_off, icmp_len;
+	uint32_t icmp_sum;   // split schedule: sum of the message words before icmp_off (fast_walk<.., true>)
 	int      leaf;       // device: a host-rendered leaf at w.data whose end is still to walk
 };
 
@@ -245,6 +246,7 @@ NSD_HD void walk_init(WalkOut &w, uint32_t caplen, int start_id)
 	w.icmp_pend = false;
 	w.icmp_off = 0;
 	w.icmp_len = 0;
+	w.icmp_sum = 0;
 	w.leaf = 0;
 }
 
@@ -547,8 +549,11 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 // Returns FW_DONE, FW_RESTART (the general walk takes the packet from its start) or
 // FW_RESUME (the chain reached an extension header / AH / IPv6-in-IPv4 ops
 // at w.data with layers 0..w.n-1 recorded: the general walk resumes there with w.id).
+// FOLD (the split schedule's fast kernel): an ICMPv4 message that runs past
+// the window has its words inside the window summed here, from LDS (w.icmp_sum),
+// and only the rest [icmp_off, icmp_off + icmp_len) left to the checksum pass.
 enum : uint32_t { FW_DONE = 0, FW_RESTART = 1, FW_RESUME = 2 };
-template <int MODE, class Src>
+template <int MODE, bool FOLD = false, class Src>
 __device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, WalkOut &w)
 {
 	uint32_t n = 0;
@@ -662,6 +667,14 @@ __device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, Wal
 					w.icmp_pend = true;
 					w.icmp_off = d2;
 					w.icmp_len = len;
+					if (FOLD) {
+						// the words inside the window summed here (kw < len >> 1:
+						// the message does not fit); the pass sums the rest
+						const uint32_t kw = s.window_bytes(d2) >> 1;
+						w.icmp_sum = s.sum16(d2, kw);
+						w.icmp_off = d2 + 2 * kw;
+						w.icmp_len = (len & ~1u) - 2 * kw;
+					}
 				} else if (calc_csum(s, d2, len >> 1)) {
 					w.flags |= NSD_F_ICMP_BAD;
 				}

@@ -75,7 +75,9 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "dissector_entry_batch_sll", "nsd_format_packet_sll", "nsd_format_batch_sll",
                "nsd_pipe_submit_sll", "nsd_pcap_read_batch_sll", "nsd_t3_block_desc_sll",
                "nsd_replay_pcap_out", "nsd_build_info", "nsd_walk_packet_cpu", "nsd_set_etcdir",
-               "nsd_dissect_device_compact", "nsd_format_batch_compact"]
+               "nsd_dissect_device_compact", "nsd_format_batch_compact", "nsd_pipe_create_compact",
+               "nsd_pipe_submit_compact", "nsd_format_range_compact", "nsd_set_schedule",
+               "nsd_last_schedule"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -193,10 +195,39 @@ def lib():
                                                  _vp, _vp]
         L.nsd_format_batch_compact.restype = ctypes.c_long
         L.nsd_format_batch_compact.argtypes = [_vp, _vp, _vp, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]
+        L.nsd_pipe_create_compact.restype = _vp
+        L.nsd_pipe_create_compact.argtypes = [_u32, _sz, _u32, _int, _int, _int]
+        L.nsd_pipe_submit_compact.restype = _int
+        L.nsd_pipe_submit_compact.argtypes = [_vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
+        L.nsd_format_range_compact.restype = ctypes.c_long
+        L.nsd_format_range_compact.argtypes = [_vp, _vp, _vp, _u32, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp,
+                                               _vp]
+        L.nsd_set_schedule.restype = _int
+        L.nsd_set_schedule.argtypes = [_int]
+        L.nsd_last_schedule.restype = _int
         L.nsd_replay_pcap.restype = ctypes.c_long
         L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp, _int]
         _lib = L
     return _lib
+
+
+SCHED_ADAPTIVE, SCHED_SPLIT, SCHED_FUSED = 0, 1, 2
+SCHED_NAMES = {0: None, 1: "split", 2: "fused"}
+
+
+def set_schedule(sched):
+    """Force the batch walks' kernel schedule (SCHED_SPLIT / SCHED_FUSED) or
+    let the library pick it (SCHED_ADAPTIVE, the default); returns the
+    previous setting."""
+    rc = lib().nsd_set_schedule(sched)
+    if rc < 0:
+        raise ValueError(f"bad schedule {sched}")
+    return rc
+
+
+def last_schedule():
+    """"split" / "fused": the schedule of the last launch (None before any)."""
+    return SCHED_NAMES.get(lib().nsd_last_schedule())
 
 
 class NsdError(RuntimeError):
@@ -361,11 +392,15 @@ class Pipe:
     submit() are kept alive until then."""
 
     def __init__(self, max_pkts, max_frame_bytes, ext_words=0, depth=3, mode=PRINT_NORM,
-                 linktype=LINKTYPE_EN10MB):
+                 linktype=LINKTYPE_EN10MB, compact=False):
+        """compact: records are nsd_crec (CREC_DTYPE) and the pool holds the
+        side words first (nsd_pipe_create_compact: ext_words >= max_pkts)."""
         self.L = lib()
-        self.p = self.L.nsd_pipe_create(max_pkts, max_frame_bytes, ext_words, depth, linktype, mode)
+        create = self.L.nsd_pipe_create_compact if compact else self.L.nsd_pipe_create
+        self.p = create(max_pkts, max_frame_bytes, ext_words, depth, linktype, mode)
         if not self.p:
             raise NsdError("nsd_pipe_create failed")
+        self.compact = compact
         self.ext_words = ext_words
         self.depth = depth
         self.inflight = []
@@ -380,10 +415,11 @@ class Pipe:
         if sll is not None:
             sll = np.ascontiguousarray(sll, dtype=SLL_DTYPE)
             assert len(sll) == n
-        rc = self.L.nsd_pipe_submit_sll(self.p, frames.ctypes.data, frames.nbytes, desc.ctypes.data,
-                                        ptr(sll), n, rec.ctypes.data, ptr(ext), ptr(ext_used),
-                                        ptr(counters), ptr(status))
-        _check(rc, "nsd_pipe_submit_sll")
+        submit = self.L.nsd_pipe_submit_compact if self.compact else self.L.nsd_pipe_submit_sll
+        assert rec.dtype == (CREC_DTYPE if self.compact else REC_DTYPE)
+        rc = submit(self.p, frames.ctypes.data, frames.nbytes, desc.ctypes.data, ptr(sll), n, rec.ctypes.data,
+                    ptr(ext), ptr(ext_used), ptr(counters), ptr(status))
+        _check(rc, "nsd_pipe_submit")
         self.inflight.append((frames, desc, rec, ext, ext_used, counters, status, sll))
         if len(self.inflight) > self.depth:   # the library completed the oldest first
             self.inflight.pop(0)

@@ -22,3 +22,14 @@ def native_build():
     if not os.path.exists(os.path.join(ROOT, "netsniff-ng_amd", "libnsdissect.so")):
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "netsniff-ng_amd")], check=True)
     yield
+
+
+@pytest.fixture(params=["split", "fused"])
+def schedule(request):
+    """Runs a parity test under both kernel schedules (nsd_set_schedule): the
+    split fast + walker kernels and the fused kernel must each match the
+    oracle; the library's adaptive choice is restored after."""
+    import nsd
+    prev = nsd.set_schedule(nsd.SCHED_SPLIT if request.param == "split" else nsd.SCHED_FUSED)
+    yield request.param
+    nsd.set_schedule(prev)

@@ -22,7 +22,7 @@ import pytest
 import nsd
 import nsd_testlib as T
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("schedule")]
 
 SHARD = 1 << 24
 SHARDS = 8

@@ -7,7 +7,7 @@ import edge_cases
 import nsd
 import nsd_testlib as T
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("schedule")]
 
 MODES = [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX]
 
@@ -250,6 +250,51 @@ def test_pipe_batches(depth):
         assert_same_records(rec, orec, ext[:int(ec[0])], oext)
         assert np.array_equal(cnt, ocnt)
     assert pipe.wait() == 1
+    pipe.close()
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_pipe_batches_compact(depth):
+    """The compact-record pipe (nsd_pipe_create_compact / _submit_compact):
+    batches of different sizes and configs in flight together (the deep
+    IPv6 chains need side words and entries, IMIX none); each batch's
+    records, side words / entries and counters equal compact_of(oracle)."""
+    specs = [(T.SYN_IMIX, 20000, 0), (T.SYN_IPV6X, 7000, 0), (T.SYN_UDP64, 1, 5),
+             (T.SYN_IPV6X, 9000, 7000), (T.SYN_IMIX, 3, 99)]
+    batches = [T.make_batch(cfg, n, lo=lo) for cfg, n, lo in specs]
+    batches.append(T.batch_from_packets(_long_chains(3000), align=2))
+    max_pkts = max(len(d) for _, d in batches)
+    max_bytes = max(f.nbytes for f, _ in batches)
+    words = max_pkts + nsd.ext_pool_words(max_pkts)
+    pipe = nsd.Pipe(max_pkts, max_bytes, ext_words=words, depth=depth, compact=True)
+    outs = []
+    for frames, desc in batches:
+        rec = np.zeros(len(desc), dtype=nsd.CREC_DTYPE)
+        ext = np.zeros(words, dtype=np.uint32)
+        ec = np.zeros(1, np.uint32)
+        cnt = np.zeros(nsd.NCOUNTERS, np.uint64)
+        st = np.full(1, -99, np.int32)
+        pipe.submit(frames, desc, rec, ext, ec, cnt, st)
+        outs.append((rec, ext, ec, cnt, st))
+    assert pipe.drain() == 0
+    for (frames, desc), (rec, ext, ec, cnt, st) in zip(batches, outs):
+        assert st[0] == 0
+        n = len(desc)
+        orec, oext, ocnt, _ = T.oracle_records(frames, desc)
+        want, wpool = nsd.compact_of(orec, oext)
+        assert np.array_equal(cnt, ocnt)
+        for fld in ("ip_csum", "nflags", "nlayers"):
+            assert np.array_equal(rec[fld], want[fld]), fld
+        deep = ((want["nflags"] & 7) == 7) & (want["nlayers"] == 0)
+        assert np.array_equal(rec["chain"][~deep], want["chain"][~deep])
+        side = want["nlayers"] != 0
+        assert np.array_equal(ext[:n][side], wpool[:n][side])
+        for i in np.nonzero(deep)[0]:
+            gp, gids, _ = nsd.ext_entry(ext, int(rec[i]["chain"]))
+            _, oids, _ = nsd.ext_entry(wpool, int(want[i]["chain"]))
+            assert gp == i and gids == oids
+        texts, rc = nsd.format_batch_compact(frames, desc, rec, ext)
+        assert (rc == 0).all()
     pipe.close()
 
 

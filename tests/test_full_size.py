@@ -18,7 +18,7 @@ import nsd
 import nsd_testlib as T
 from test_device_parity import _chain
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("schedule")]
 
 N = 1 << 24
 

@@ -42,6 +42,7 @@ def test_fuzz_formatter_vs_reference(tmp_path, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.usefixtures("schedule")
 @pytest.mark.parametrize("mode,align", [(T.PRINT_NORM, 16), (T.PRINT_LESS, 16), (T.PRINT_NORM, 1)])
 def test_fuzz_device_vs_oracle(mode, align):
     from test_device_parity import assert_same_records

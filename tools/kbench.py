@@ -7,7 +7,6 @@ Not the benchmark (bench.py is).
 """
 import argparse
 import os
-import shutil
 import sys
 
 import numpy as np
@@ -28,7 +27,13 @@ def main():
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--records", default="both", choices=["compact", "full", "both"])
+    ap.add_argument("--lib", default=None, help="a variant libnsdissect.so (tools/build_variant.sh) "
+                    "loaded instead of the in-tree one (dev tools only; the product loads its own)")
     args = ap.parse_args()
+    import nsd
+    if args.lib:
+        nsd.LIB_PATH = os.path.abspath(args.lib)
+    print(f"library {os.path.relpath(nsd.LIB_PATH, ROOT)}", flush=True)
     import bench
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)

@@ -14,14 +14,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PACKETS = 1 << 24
 
 
-def counters(cfg):
-    per = collections.defaultdict(list)
+def counters(cfg, kernels=("dissect_all<0, true>", "dissect_fast<0, true>", "dissect_walk<0, true>")):
+    """Per-launch counter values: each kernel's average over its dispatches,
+    summed over the kernels of one launch (dissect_fast + dissect_walk, or
+    dissect_all)."""
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(ROOT, "gpurun_out", "pmc", f"{cfg}_*", "**", "*counter_collection.csv"),
                        recursive=True):
         for r in csv.DictReader(open(f)):
-            if "dissect_all<0, true>" in r["Kernel_Name"]:
-                per[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in per.items()}
+            name = next((k for k in kernels if k in r["Kernel_Name"]), None)
+            if name:
+                per[r["Counter_Name"]][name].append(float(r["Counter_Value"]))
+    return {k: sum(sum(v) / len(v) for v in byk.values()) for k, byk in per.items()}
 
 
 def summary(cfg):
