@@ -127,6 +127,10 @@ typedef struct nsd_rec {
                                       types); data_off is still where that parser's pulls end */
 #define NSD_F_OVERFLOW       0x20  /* chain longer than NSD_EXT_MAX_LAYERS or ext pool full:
                                       record holds the first layers only */
+#define NSD_F_LEAF_END       0x40  /* compact records (nsd_crec) of an NSD_F_HOST leaf: where the
+                                      leaf's pulls end (the 16-byte record's data_off) is in the
+                                      packet's side word (chains up to 6 layers) or in word 2 of
+                                      its ext entry (chains past 12 layers), bits 0..15 */
 
 #define NSD_REC_NLAYERS(r)   ((r)->nflags & 7u)
 #define NSD_REC_ID(r, k)     (((r)->chain >> (5u * (k))) & 31u)
@@ -405,6 +409,10 @@ int nsd_walk_packet_cpu(const uint8_t *pkt, uint32_t caplen, int linktype, int m
  *  - longer chains: chain = the ext pool slot (0xFFFFFFFF with
  *    NSD_F_OVERFLOW: pool full), nflags & 7 = NSD_N_EXT, nlayers = 0; the
  *    entry keeps the ids (offset bits 0: no cursors in this form either).
+ * Host-rendered leaves (NSD_F_HOST) also get their end cursor when the pool
+ * has side words: NSD_F_LEAF_END, the cursor in the side word (up to 6
+ * layers) or in the entry's word 2 (past 12 layers; a 7..12-layer chain's
+ * side word holds ids, so its leaf has no recorded end).
  * nflags (besides the count), ip_csum: as in nsd_rec.  The counters are the
  * same as for 16-byte records (NSD_CNT_EXT counts the chains that need the
  * 16-byte record's ext form). */

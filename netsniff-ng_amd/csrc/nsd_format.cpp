@@ -1015,7 +1015,7 @@ static bool format_no_chain(Out &o, const Frame &f, uint32_t caplen, int mode)
 // final {data, tail} to check, or NULL.
 static int format_chain(Out &o, const Frame &f, int linktype, int mode, uint32_t n, const uint8_t *ids,
 			const uint16_t *offs, const uint32_t *end, uint16_t ip_csum, uint8_t nflags,
-			const nsd_sll_t *sll)
+			const nsd_sll_t *sll, uint32_t leaf_end = 0xFFFFFFFFu)
 {
 	const bool host = nflags & NSD_F_HOST;
 	if (n == 0 && is_lt(linktype, NSD_LINKTYPE_EN10MB))
@@ -1038,6 +1038,9 @@ static int format_chain(Out &o, const Frame &f, int linktype, int mode, uint32_t
 				return NSD_ERR_FORMAT;
 		} else {
 			if (dn.next || (end && (dn.data != end[0] || dn.tail != end[1])))
+				return NSD_ERR_FORMAT;
+			// compact records: the device's end of a host-rendered leaf
+			if (leaf_end != 0xFFFFFFFFu && dn.data != leaf_end)
 				return NSD_ERR_FORMAT;
 		}
 		tail = dn.tail;
@@ -1120,15 +1123,20 @@ int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, i
 								  : (ext_pool[i] >> (5 * (k - NSD_REC_MAX_LAYERS))) & 31);
 		return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll);
 	}
+	const bool le = (rec.nflags & (NSD_F_HOST | NSD_F_LEAF_END)) == (NSD_F_HOST | NSD_F_LEAF_END);
+	if (le && !ext_pool)
+		return NSD_ERR_FORMAT;
 	if (n == NSD_N_EXT) {
-		// (a compact chain's entry holds ids only)
+		// (a compact chain's entry holds ids only; a host leaf's end in word 2)
 		if (ext_chain(ext_pool, rec.chain, rec.nflags, n, ids, offs) != NSD_OK)
 			return NSD_ERR_FORMAT;
-		return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll);
+		return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll,
+				    le ? ext_pool[rec.chain + 2] & 0xFFFF : 0xFFFFFFFFu);
 	}
 	for (uint32_t k = 0; k < n; k++)
 		ids[k] = (uint8_t)((rec.chain >> (5 * k)) & 31);
-	return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll);
+	return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll,
+			    le ? ext_pool[i] & 0xFFFF : 0xFFFFFFFFu);
 }
 
 // hex() / ascii() / hex_ascii() over [from, to) (proto_none.c:28-72)

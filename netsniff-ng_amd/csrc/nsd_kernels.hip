@@ -521,10 +521,16 @@ struct Pending {
 	uint32_t npend, nleaf;
 };
 
-// leaf entry: packet index | leaf start << 32 | ops id << 48
+// leaf entry: packet index | leaf start << 32 | ops id << 48 (16-byte
+// records), packet index | leaf start << 32 | tail << 48 (compact records,
+// whose record has no tail; the id is the chain's last)
 __device__ __forceinline__ uint64_t leaf_entry(uint32_t i, uint32_t start, int id)
 {
 	return (uint64_t)i | (uint64_t)(start & 0xFFFF) << 32 | (uint64_t)id << 48;
+}
+__device__ __forceinline__ uint64_t leaf_entry_c(uint32_t i, uint32_t start, uint32_t tail)
+{
+	return (uint64_t)i | (uint64_t)(start & 0xFFFF) << 32 | (uint64_t)(tail & 0xFFFF) << 48;
 }
 
 // What a lane whose general walk ended leaves behind (wave-uniform call):
@@ -540,11 +546,19 @@ template <int MODE, bool CR>
 __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, uint32_t caplen, const GenSink<CR> &g,
 					     void *__restrict__ rec, Pending &pq, FlagCnt &fc, int lane)
 {
-	// (the compact record has no cursor for the leaf pass to set)
-	const bool lf = !CR && fin && w.leaf != 0;
+	// a host-rendered leaf's end is walked by the leaf pass: into the 16-byte
+	// record's cursor, or (compact records with side words) into the side
+	// word of a chain of up to 6 layers or word 2 of an entry past 12 layers
+	const bool lf = fin && w.leaf != 0 &&
+			(!CR || (g.side && (w.n <= NSD_REC_MAX_LAYERS || (w.ext_on && w.slot != 0xFFFFFFFFu &&
+									   w.n <= NSD_EXT_MAX_LAYERS))));
 	const uint64_t lm = __ballot(lf);
-	if (lf)
-		pq.wq[pq.wcap - 1 - (pq.nleaf + lanes_below(lm))] = leaf_entry(i, w.data, w.leaf);
+	if (lf) {
+		pq.wq[pq.wcap - 1 - (pq.nleaf + lanes_below(lm))] =
+			CR ? leaf_entry_c(i, w.data, w.tail) : leaf_entry(i, w.data, w.leaf);
+		if (CR)
+			w.flags |= NSD_F_LEAF_END;
+	}
 	pq.nleaf += (uint32_t)__popcll(lm);
 	uint64_t *const wq = pq.wq;
 	uint32_t &npend = pq.npend;
@@ -866,6 +880,11 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 						key = 0xFFFFFFFFu;
 				}
 			}
+			if (CR && g.side && done && (w.flags & NSD_F_HOST)) {
+				// a leaf the fast walk finished (ARP, DCCP): its end in the side word
+				g.side[i] = w.data;
+				w.flags |= NSD_F_LEAF_END;
+			}
 			if (done)
 				put_rec<CR>(rec, i, w);
 			fc.add(w, caplen, done);
@@ -996,9 +1015,9 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 // (nsd_leaf.h) and rewrites the record's cursor word.  A pass of its own,
 // after the tiles, so the LLDP TLV and ND-option loops do not add to the
 // walk's register peak.  The wave reads back only what it wrote itself.
-template <int MODE>
+template <int MODE, bool CR>
 __device__ __forceinline__ void leaf_pass(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc,
-					  uint4 *__restrict__ rec, const Pending &pq)
+					  void *__restrict__ rec, uint32_t *__restrict__ pool, const Pending &pq)
 {
 	if (!pq.nleaf)
 		return;
@@ -1006,13 +1025,33 @@ __device__ __forceinline__ void leaf_pass(const uint8_t *__restrict__ frames, co
 	for (uint32_t k = threadIdx.x & 63; k < pq.nleaf; k += 64) {
 		const uint64_t e = pq.wq[pq.wcap - 1 - k];
 		const uint32_t i = (uint32_t)e, start = (uint32_t)(e >> 32) & 0xFFFF;
-		const int id = (int)(e >> 48);
 		const uint64_t d = desc[i];
-		uint32_t *const y = (uint32_t *)(rec + i) + 1;   // data_off | tail_off << 16
-		const uint32_t tail = __hip_atomic_load(y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16;
-		const uint32_t end =
-			leaf_end<MODE>(HbmBytes{ frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d) }, id, start, tail);
-		*y = end | tail << 16;
+		const HbmBytes src{ frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d) };
+		if constexpr (!CR) {
+			const int id = (int)(e >> 48);
+			uint32_t *const y = (uint32_t *)((uint4 *)rec + i) + 1;   // data_off | tail_off << 16
+			const uint32_t tail = __hip_atomic_load(y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16;
+			*y = leaf_end<MODE>(src, id, start, tail) | tail << 16;
+		} else {
+			// the leaf is the chain's last layer: its id from the record (inline
+			// ids) or the entry (ids only); its end into the side word or entry
+			const uint32_t tail = (uint32_t)(e >> 48);
+			const uint64_t rv = __hip_atomic_load((uint64_t *)rec + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			const uint2 r = make_uint2((uint32_t)rv, (uint32_t)(rv >> 32));
+			const uint32_t nf = (r.y >> 16) & 0xFF, n = nf & 7;
+			uint32_t *loc;
+			int id;
+			if (n != NSD_N_EXT) {
+				id = (int)((r.x >> (5 * (n - 1))) & 31);
+				loc = pool + i;
+			} else {
+				const uint32_t nl = __hip_atomic_load(pool + r.x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFFF;
+				id = (int)(__hip_atomic_load(pool + r.x + NSD_EXT_HDR_WORDS + nl - 1, __ATOMIC_RELAXED,
+							     __HIP_MEMORY_SCOPE_AGENT) & 31);
+				loc = pool + r.x + 2;
+			}
+			*loc = leaf_end<MODE>(src, id, start, tail);
+		}
 	}
 }
 
@@ -1041,8 +1080,8 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	Pending pq{ pend + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (region / WAVES), region / WAVES, 0,
 		    0 };
 	walk_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq);
-	if (!CR && (MODE == PRINT_NORM || MODE == PRINT_LESS))
-		leaf_pass<MODE>(frames, desc, (uint4 *)rec, pq);
+	if (MODE == PRINT_NORM || MODE == PRINT_LESS)
+		leaf_pass<MODE, CR>(frames, desc, rec, ext, pq);
 	if ((threadIdx.x & 63) == 0)
 		sh.pcnt[threadIdx.x >> 6] = pq.npend;
 	if (MODE == PRINT_NORM) {
@@ -1134,8 +1173,8 @@ __device__ __forceinline__ uint32_t fold_weighted(uint32_t sum, bool odd)
 template <int MODE, bool CR>
 __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__restrict__ frames,
 					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
-					   void *__restrict__ rec, const uint32_t *__restrict__ sll, uint4 *__restrict__ list,
-					   uint32_t cap, uint32_t &ndef, uint32_t &nicmp)
+					   void *__restrict__ rec, const uint32_t *__restrict__ sll, uint32_t *__restrict__ side,
+					   uint4 *__restrict__ list, uint32_t cap, uint32_t &ndef, uint32_t &nicmp)
 {
 	constexpr int SW = 2;
 	const int lane = threadIdx.x & 63;
@@ -1234,6 +1273,11 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 				if (key == lk)
 					key = 0xFFFFFFFFu;
 			}
+		}
+		if (CR && side && done && (w.flags & NSD_F_HOST)) {
+			// a leaf the fast walk finished (ARP, DCCP): its end in the side word
+			side[i] = w.data;
+			w.flags |= NSD_F_LEAF_END;
 		}
 		if (done)
 			put_rec<CR>(rec, i, w);
@@ -1354,7 +1398,7 @@ template <int MODE, bool CR>
 __global__ __launch_bounds__(BLOCK, NSD_FAST_MINW) void dissect_fast(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 	void *__restrict__ rec, unsigned long long *__restrict__ counters, uint4 *__restrict__ lists, uint32_t cap,
-	uint2 *__restrict__ cnts, const uint32_t *__restrict__ sll)
+	uint2 *__restrict__ cnts, const uint32_t *__restrict__ sll, uint32_t *__restrict__ side)
 {
 	constexpr int SW = 2;
 	__shared__ FastShared sh;
@@ -1364,7 +1408,8 @@ __global__ __launch_bounds__(BLOCK, NSD_FAST_MINW) void dissect_fast(
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 	const uint32_t gw = blockIdx.x * WAVES + wv;
 	uint32_t ndef = 0, nicmp = 0;
-	fast_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, sll, lists + (size_t)gw * cap * SW, cap, ndef, nicmp);
+	fast_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, sll, side, lists + (size_t)gw * cap * SW, cap, ndef,
+			     nicmp);
 	if (lane == 0) {
 		cnts[gw] = make_uint2(ndef, nicmp);
 		sh.pcnt[wv] = nicmp;
@@ -1509,8 +1554,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
 			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, none, pw, 0, 0, true);
 	}
 	fc.flush(sh.cnt, lane);
-	if (!CR)
-		leaf_pass<MODE>(frames, desc, (uint4 *)rec, pq);
+	leaf_pass<MODE, CR>(frames, desc, rec, ext, pq);
 	if (lane == 0)
 		sh.pcnt[wv] = pq.npend;
 	if (MODE == PRINT_NORM) {
@@ -1747,7 +1791,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	return 0;
 	}
 	typedef void (*ffn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, unsigned long long *, uint4 *,
-			    uint32_t, uint2 *, const uint32_t *);
+			    uint32_t, uint2 *, const uint32_t *, uint32_t *);
 	typedef void (*wfn)(const uint8_t *, const uint64_t *, uint32_t, void *, uint32_t *, uint32_t, uint32_t *,
 			    uint32_t, unsigned long long *, const uint4 *, uint32_t, const uint2 *, uint32_t, uint64_t *,
 			    uint32_t);
@@ -1773,8 +1817,10 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	uint4 *lists = (uint4 *)ws;
 	uint2 *cnts = (uint2 *)(ws + align256(slotb * nlists * cap));
 	uint64_t *pend = (uint64_t *)((uint8_t *)cnts + align256((size_t)nlists * 8));
+	// compact records: the pool's side words (when it has them), for leaf ends
+	uint32_t *side = compact && d_ext && ext_words >= n ? d_ext : nullptr;
 	hipLaunchKernelGGL(fast[ci][mi], dim3(fblocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec,
-			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll);
+			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll, side);
 	if (hipGetLastError() != hipSuccess)
 		return -2;
 	if (mi == 2)

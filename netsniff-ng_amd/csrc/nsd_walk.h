@@ -553,6 +553,11 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 // the window has its words inside the window summed here, from LDS (w.icmp_sum),
 // and only the rest [icmp_off, icmp_off + icmp_len) left to the checksum pass.
 enum : uint32_t { FW_DONE = 0, FW_RESTART = 1, FW_RESUME = 2 };
+// the most layers a deferred packet carries into the general walk: the SLL
+// head, Ethernet, two tags (the loop below) and IP.  The hand-over packs the
+// layer count into 3 bits and the next ops id into 5 (take(), fast_tiles).
+constexpr uint32_t FW_MAX_LAYERS = 5;
+static_assert(FW_MAX_LAYERS < 8 && NSD_OPS_COUNT <= 32, "a deferred walk state packs n in 3 bits and id in 5");
 template <int MODE, bool FOLD = false, class Src>
 __device__ __forceinline__ uint32_t fast_walk(const Src &s, uint32_t caplen, WalkOut &w)
 {

@@ -20,6 +20,7 @@ NCOUNTERS = 64
 NSD_OPS_COUNT = 28
 CNT_PKTS, CNT_BYTES, CNT_IP_BAD, CNT_ICMP_BAD, CNT_HOST, CNT_EXT, CNT_OVERFLOW, CNT_TRIM = range(32, 40)
 FRAME_PAD = 64
+F_ICMP_BAD, F_HOST, F_OVERFLOW, F_LEAF_END = 0x08, 0x10, 0x20, 0x40
 
 REC_DTYPE = np.dtype([("chain", "<u4"), ("data_off", "<u2"), ("tail_off", "<u2"),
                       ("ip_csum", "<u2"), ("nflags", "u1"), ("off2", "u1", (5,))])
@@ -315,9 +316,16 @@ def compact_of(rec, ext=None):
     out = np.zeros(n, dtype=CREC_DTYPE)
     side = np.zeros(n, dtype=np.uint32)
     src = np.zeros(0, dtype=np.uint32) if ext is None else np.asarray(ext).view(np.uint32)
+    src = src.copy()
     out["chain"] = rec["chain"]
     out["ip_csum"] = rec["ip_csum"]
     out["nflags"] = rec["nflags"]
+    # a host-rendered leaf (NSD_F_HOST) keeps its end (data_off) in the side
+    # word of an inline chain, or in word 2 of an entry (NSD_F_LEAF_END)
+    host = ((rec["nflags"] & F_HOST) != 0) & ((rec["nflags"] & F_OVERFLOW) == 0)
+    inline = host & ((rec["nflags"] & 7) != 7)
+    side[inline] = rec["data_off"][inline]
+    out["nflags"][inline] |= F_LEAF_END
     slots = rec["off2"][:, :4].copy().view("<u4").reshape(-1)
     for i in np.nonzero((rec["nflags"] & 7) == 7)[0]:
         s, flags = int(slots[i]), int(rec[i]["nflags"]) & 0xF8
@@ -327,10 +335,15 @@ def compact_of(rec, ext=None):
         _, ids, _ = ext_entry(src, s)
         if len(ids) > 12:
             out[i]["chain"] = s + n
+            if host[i]:
+                src[s + 2] = rec[i]["data_off"]
+                out[i]["nflags"] |= F_LEAF_END
             continue
         out[i]["chain"] = sum(ids[k] << (5 * k) for k in range(min(len(ids), 6)))
         if len(ids) <= 6:                    # ext form only for an offset past 510
-            out[i]["nflags"] = len(ids) | flags
+            out[i]["nflags"] = len(ids) | flags | (F_LEAF_END if host[i] else 0)
+            if host[i]:
+                side[i] = rec[i]["data_off"]
         else:
             out[i]["nlayers"] = len(ids)
             side[i] = sum(ids[k] << (5 * (k - 6)) for k in range(6, len(ids)))

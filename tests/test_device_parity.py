@@ -102,7 +102,9 @@ def _check_compact(frames, desc, mode):
         assert len(bad) == 0, f"{fld} differs at {bad[:10]}"
     deep = ((want["nflags"] & 7) == 7) & (want["nlayers"] == 0)
     assert np.array_equal(got["chain"][~deep], want["chain"][~deep]), "chain ids differ"
-    side = want["nlayers"] != 0
+    # side words: ids 6.. of 7..12-layer chains, or a host leaf's end (NSD_F_LEAF_END)
+    leaf = (want["nflags"] & nsd.F_LEAF_END) != 0
+    side = (want["nlayers"] != 0) | (leaf & ~deep)
     assert np.array_equal(dpool[:n][side], wpool[:n][side]), "side words differ"
     for i in np.nonzero(deep)[0]:
         if want[i]["chain"] == 0xFFFFFFFF:      # no entry (pool full)
@@ -111,15 +113,31 @@ def _check_compact(frames, desc, mode):
         gp, gids, goffs = nsd.ext_entry(dpool, int(got[i]["chain"]))
         _, oids, _ = nsd.ext_entry(wpool, int(want[i]["chain"]))
         assert gp == i and gids == oids and not any(goffs), f"ext chain differs at {i}"
+        if leaf[i]:
+            assert dpool[int(got[i]["chain"]) + 2] == wpool[int(want[i]["chain"]) + 2], f"leaf end differs at {i}"
     assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt)
     return got, dpool
 
 
 @pytest.mark.parametrize("mode", MODES)
 def test_compact_edge_and_leaves(mode):
+    """Compact records of the edge cases and the leaf set: the host-rendered
+    leaves' ends (NSD_F_LEAF_END in side words / entries) equal the oracle's
+    data_off, which the reference text pins (tests/golden/leaves.*), and the
+    formatter renders every record with its leaf end checked."""
     _, leaves = T.read_pcap(T.GOLDEN + "/leaves.pcap")
     frames, desc = T.batch_from_packets(edge_cases.cases() + leaves, align=2)
-    _check_compact(frames, desc, mode)
+    got, pool = _check_compact(frames, desc, mode)
+    if mode in (T.PRINT_NORM, T.PRINT_LESS):
+        assert ((got["nflags"] & nsd.F_LEAF_END) != 0).sum() >= 2000
+        texts, rc = nsd.format_batch_compact(frames, desc, got, pool, mode=mode)
+        assert ((rc == 0) | ((got["nflags"] & nsd.F_OVERFLOW) != 0)).all()   # overflow: per-packet path
+        # a wrong leaf end is refused
+        k = int(np.nonzero(((got["nflags"] & nsd.F_LEAF_END) != 0) & ((got["nflags"] & 7) != 7))[0][0])
+        bad = pool.copy()
+        bad[k] ^= 1
+        _, rc2 = nsd.format_batch_compact(frames, desc, got, bad, mode=mode)
+        assert rc2[k] != 0
 
 
 @pytest.mark.parametrize("cfg", [T.SYN_UDP64, T.SYN_IMIX, T.SYN_IPV6X])
