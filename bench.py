@@ -284,16 +284,24 @@ def time_steps(b, mode, steps, warmup, grid=0):
 
 
 # ---- in-run PMC traffic ----------------------------------------------------------
+PMC_WARM = 80   # launches per config before the counted ones: the adaptive schedule settles
+
+
 def pmc_child(args):
-    """Runs under rocprofv3 --pmc: `steps` dissect launches per config, in
-    the order of --pmc-configs (the parent splits the dispatches by order)."""
+    """Runs under rocprofv3 --pmc: PMC_WARM + `steps` dissect launches per
+    config, in the order of --pmc-configs (the parent splits the dispatches
+    by order and counts the last `steps` of each config: by then the adaptive
+    schedule is the one the timed run uses)."""
     torch.cuda.set_device(0)
     for key in args.pmc_configs.split(","):
         shards = args.shards if key == args.config else 1
         b = Batch(key, args.packets, 0, shards, torch.device("cuda", 0), compact=args.records == "compact")
-        for _ in range(args.steps):
+        for k in range(PMC_WARM + args.steps):
             b.step(args.mode, args.grid)
+            if k % 16 == 15:
+                torch.cuda.synchronize()
         torch.cuda.synchronize()
+        print(f"pmc-child {key} schedule {nsd.last_schedule()}", flush=True)
         b.free()
         torch.cuda.empty_cache()
 
@@ -334,10 +342,11 @@ def pmc_traffic(args, keys, steps=3):
                     launches[-1] += v
                 else:
                     launches.append(v)
-            if len(launches) != steps * len(keys):
-                return {"error": f"{ctr}: {len(launches)} dissect launches, expected {steps * len(keys)}"}
+            per = PMC_WARM + steps
+            if len(launches) != per * len(keys):
+                return {"error": f"{ctr}: {len(launches)} dissect launches, expected {per * len(keys)}"}
             for i, key in enumerate(keys):
-                v = launches[i * steps:(i + 1) * steps]
+                v = launches[(i + 1) * per - steps:(i + 1) * per]
                 got.setdefault(key, {})[ctr] = sum(v) / len(v) * 1024
     out = {}
     for key in keys:
@@ -361,7 +370,29 @@ def cpu_info():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    return model, os.cpu_count() or 1, avail
+    return model, os.cpu_count() or 1, min(avail, cpu_quota() or avail)
+
+
+def cpu_quota():
+    """CPUs this process may use by its cgroup's CFS quota (v2 cpu.max or v1
+    cfs_quota_us / cfs_period_us), None when unlimited: the GPU boxes show
+    every core of the machine but grant each GPU's jobs a 16-CPU share."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                return max(1, int(int(q) // int(per)))
+            return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return max(1, q // per) if q > 0 else None
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_rate(cfg, n_sample, threads, seconds, text):
@@ -398,19 +429,23 @@ def cpu_baseline(key, seconds):
     cfg = CONFIGS[key]["cfg"]
     model, nproc, avail = cpu_info()
     t16 = min(avail, 16)   # the GPU box's CPU share per GPU is 16 threads
-    legs = 6
+    more = avail > t16   # every available core is more than the 16-thread share
+    legs = 6 if more else 4
     t1, p1, d1 = cpu_rate(cfg, 1 << 16, 1, seconds / legs, True)
     tS, pS, dS = cpu_rate(cfg, 1 << 20, t16, seconds / legs, True)
-    tA, pA, dA = cpu_rate(cfg, max(1 << 20, 4096 * avail), avail, seconds / legs, True)
     f1, q1, e1 = cpu_rate(cfg, 1 << 20, 1, seconds / legs, False)
     fS, qS, eS = cpu_rate(cfg, 1 << 22, t16, seconds / legs, False)
-    fA, qA, eA = cpu_rate(cfg, max(1 << 22, 65536 * avail), avail, seconds / legs, False)
+    if more:
+        tA, pA, dA = cpu_rate(cfg, max(1 << 20, 4096 * avail), avail, seconds / legs, True)
+        fA, qA, eA = cpu_rate(cfg, max(1 << 22, 65536 * avail), avail, seconds / legs, False)
+    else:
+        tA, pA, dA, fA = tS, pS, dS, fS
     return {"value": round(tA, 3), "unit": "Mpkt/s", "cores": avail, "kind": "port",
             "sample": f"{key}: fields + PRINT_NORM text (the reference prints as it parses) by the CPU "
                       f"restatement (oracle/nsd_oracle.c), {avail} threads (every available core) over "
                       f"contiguous shards, {pA} packets (passes over a resident "
-                      f"{max(1 << 20, 4096 * avail)}-packet sample) in {dA:.1f} s",
-            "cpu_model": model, "nproc": nproc, "cpus_available": avail,
+                      f"{max(1 << 20, 4096 * avail) if more else 1 << 20}-packet sample) in {dA:.1f} s",
+            "cpu_model": model, "nproc": nproc, "cpus_available": avail, "cgroup_cpu_quota": cpu_quota(),
             "text_1thread": round(t1, 3),
             "text_16threads": {"threads": t16, "value": round(tS, 3)},
             "fields_only": {"all_cores": round(fA, 3), "threads16": round(fS, 3), "1thread": round(f1, 3)},
@@ -686,6 +721,7 @@ def main():
     compact = args.records == "compact"
 
     b, m = measure_rank(args, rank, world, dev)
+    schedule = nsd.last_schedule()   # the kernel schedule the timed launches ran (adaptive)
     elapsed, kern_ms, total_pkts = m["elapsed"], m["kern_ms"], m["total_pkts"]
     ms_per_step = elapsed / args.steps * 1e3
     mpps = total_pkts * args.steps / elapsed / 1e6
@@ -716,7 +752,7 @@ def main():
         lc = lb.counters.cpu().numpy().view(np.uint64)
         assert int(lc[nsd.CNT_PKTS]) == lb.n, f"{key}: counter check failed"
         ltr = traffic.get(key) if isinstance(traffic, dict) else None
-        leg_out[key] = {"workload": CONFIGS[key]["name"], "packets": lb.n,
+        leg_out[key] = {"workload": CONFIGS[key]["name"], "packets": lb.n, "schedule": nsd.last_schedule(),
                         "value": round(lb.n / (ms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
                         "gbps_frames": round(lb.frame_bytes / (ms * 1e-3) / 1e9, 1),
                         "roofline": lb.roofline(ms, ltr, copy_gbs)}
@@ -749,7 +785,7 @@ def main():
             "config": {"workload": workload_name(args.config, n, args.shards), "packets_per_gpu": b.n,
                        "frame_bytes_per_gpu": frame_bytes, "mode": MODES[args.mode],
                        "records": "compact 8 B (nsd_crec)" if compact else "full 16 B (nsd_rec)",
-                       "parallelism": f"dp{world}"},
+                       "schedule": schedule, "parallelism": f"dp{world}"},
             "gbps_frames": round(frame_bytes * world * args.steps / elapsed / 1e9, 1),
             "roofline": roofline,
             "counters_total": int(m["counters"][nsd.CNT_PKTS]),

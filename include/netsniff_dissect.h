@@ -460,8 +460,9 @@ int nsd_last_schedule(void);
  * max_pkts + the entries (its words [0, n) are the batch's side words).
  * nsd_pipe_submit_compact as nsd_pipe_submit_sll with crec[n]: ext[0, n +
  * *ext_used) receives the side words and the entries only when a record of
- * the batch needs either (its counters[NSD_CNT_EXT] > 0; otherwise ext is
- * left as it was).  Each submit form refuses the other kind of pipe. */
+ * the batch needs either (its counters[NSD_CNT_EXT] or [NSD_CNT_HOST] > 0;
+ * otherwise ext is left as it was).  Each submit form refuses the other kind
+ * of pipe. */
 nsd_pipe *nsd_pipe_create_compact(uint32_t max_pkts, size_t max_frame_bytes, uint32_t ext_words,
 				  int depth, int linktype, int mode);
 int nsd_pipe_submit_compact(nsd_pipe *p, const uint8_t *frames, size_t frames_len,

@@ -1117,7 +1117,10 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 
 constexpr int FROW = WIN1 / 4;   // fast rows: 16 dwords, 16-byte slots XOR-swizzled by swz_of(q, 4)
 #ifndef NSD_FAST_MINW
-#define NSD_FAST_MINW 6          // waves per SIMD dissect_fast is register-allocated for
+#define NSD_FAST_MINW 6          // waves per SIMD dissect_fast is register-allocated for (compact records)
+#endif
+#ifndef NSD_FAST_MINW_FULL
+#define NSD_FAST_MINW_FULL 5     // the same for 16-byte records (the deferral entries carry layer starts)
 #endif
 #ifndef NSD_FAST_PREF
 #define NSD_FAST_PREF 2          // where the next tile's chunk loads are issued (fast_tiles)
@@ -1395,7 +1398,7 @@ __device__ __forceinline__ void fast_icmp_pass(FastShared &sh, const uint8_t *__
 }
 
 template <int MODE, bool CR>
-__global__ __launch_bounds__(BLOCK, NSD_FAST_MINW) void dissect_fast(
+__global__ __launch_bounds__(BLOCK, CR ? NSD_FAST_MINW : NSD_FAST_MINW_FULL) void dissect_fast(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 	void *__restrict__ rec, unsigned long long *__restrict__ counters, uint4 *__restrict__ lists, uint32_t cap,
 	uint2 *__restrict__ cnts, const uint32_t *__restrict__ sll, uint32_t *__restrict__ side)
@@ -1601,7 +1604,7 @@ static size_t region_slots(uint32_t n)
 // traffic mix changes slowly against batches of a few milliseconds; both
 // schedules give identical results.  nsd_set_schedule forces one (tests).
 #ifndef NSD_SCHED_SAMPLE
-#define NSD_SCHED_SAMPLE 16
+#define NSD_SCHED_SAMPLE 32
 #endif
 namespace {
 constexpr int MAX_DEV = 16;

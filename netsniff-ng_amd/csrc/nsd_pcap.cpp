@@ -51,6 +51,8 @@ void cpu_count_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mod
 		      uint64_t *counters);
 }
 
+extern "C" __attribute__((visibility("hidden"))) int nsd_pipe_retarget(nsd_pipe *p, int linktype, int mode);
+
 namespace {
 
 constexpr uint32_t TCPDUMP = 0xa1b2c3d4, NSEC = 0xa1b23c4d, KUZ = 0xa1b2cd34, BKM = 0xa1e2cb12;
@@ -359,6 +361,62 @@ static bool push_fhdr(const nsd_pcap *p, int fd)
 	return write_all(fd, h, sizeof(h));
 }
 
+// The replay's staging: pinned host buffers per batch slot and the device pipe.
+namespace {
+constexpr uint32_t BATCH = 1u << 16;
+constexpr size_t FRAME_BYTES = 32ull << 20;
+constexpr int DEPTH = 3;           // batches on the device
+constexpr int NSLOT = DEPTH + 3;   // + being rendered, rendered, being written
+// the side words and room for a quarter of a batch to take a deep (> 12
+// layer) entry; a chain the pool cannot hold is rendered per packet
+constexpr uint32_t EXT_WORDS = BATCH + BATCH / 4 * NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS);
+
+struct ReplayRes {
+	nsd_pipe *pipe = nullptr;
+	struct {
+		uint8_t *frames;
+		nsd_desc_t *desc;
+		nsd_sll_t *sll;
+		nsd_crec *rec;
+		uint32_t *ext;
+	} buf[NSLOT] = {};
+	bool ready() const { return pipe != nullptr; }
+	long create(int lt, int mode)
+	{
+		pipe = nsd_pipe_create_compact(BATCH, FRAME_BYTES, EXT_WORDS, DEPTH, lt, mode);
+		if (!pipe)
+			return NSD_ERR_HIP;
+		for (auto &x : buf) {
+			x.frames = (uint8_t *)nsd_host_alloc(FRAME_BYTES);
+			x.desc = (nsd_desc_t *)nsd_host_alloc(BATCH * sizeof(nsd_desc_t));
+			x.sll = (nsd_sll_t *)nsd_host_alloc(BATCH * sizeof(nsd_sll_t));
+			x.rec = (nsd_crec *)nsd_host_alloc(BATCH * sizeof(nsd_crec));
+			x.ext = (uint32_t *)nsd_host_alloc(EXT_WORDS * sizeof(uint32_t));
+			if (!x.frames || !x.desc || !x.sll || !x.rec || !x.ext) {
+				release();
+				return NSD_ERR_NOMEM;
+			}
+		}
+		return NSD_OK;
+	}
+	void release()
+	{
+		for (auto &x : buf) {
+			nsd_host_free(x.frames);
+			nsd_host_free(x.desc);
+			nsd_host_free(x.sll);
+			nsd_host_free(x.rec);
+			nsd_host_free(x.ext);
+			x = {};
+		}
+		nsd_pipe_destroy(pipe);
+		pipe = nullptr;
+	}
+};
+std::mutex g_replay_mu;
+ReplayRes g_replay;
+} // namespace
+
 // As nsd_replay_pcap; with pcap_fd >= 0 also the `--out f.pcap` write-out
 // of read_pcap (netsniff-ng.c:636, 693-697, 739-746): the file header, then
 // every record that passed the filter exactly as it was read (record header
@@ -386,27 +444,28 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	}
 	if (threads > 64)
 		threads = 64;
-	constexpr uint32_t BATCH = 1u << 16;
-	constexpr size_t FRAME_BYTES = 32ull << 20;
-	constexpr int DEPTH = 3;           // batches on the device
-	constexpr int NSLOT = DEPTH + 3;   // + being rendered, rendered, being written
 	nsd_pcap *p = nsd_pcap_open(path);
 	if (!p)
 		return NSD_ERR_ARG;
 	const int lt = (int)p->linktype;
 	const bool has_ll = p->ll_extra != 0;   // *_LL file: one sockaddr_ll per record
-	// the side words and room for a quarter of the batch to take a deep (> 12
-	// layer) entry; a chain the pool cannot hold is rendered per packet (below)
-	const uint32_t ext_words = BATCH + BATCH / 4 * NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS);
 	if (pcap_fd >= 0 && !push_fhdr(p, pcap_fd)) {
 		nsd_pcap_close(p);
 		return NSD_ERR_ARG;
 	}
-	nsd_pipe *pipe = nsd_pipe_create_compact(BATCH, FRAME_BYTES, ext_words, DEPTH, lt, mode);
-	if (!pipe) {
+	// the pinned staging and the device pipe (hundreds of MB: their set-up
+	// costs about as much as replaying a million records) are kept for the
+	// process and reused by the next replay; a replay running beside another
+	// gets its own
+	std::unique_lock<std::mutex> cache_lk(g_replay_mu, std::try_to_lock);
+	ReplayRes own;
+	ReplayRes &res = cache_lk.owns_lock() ? g_replay : own;
+	long rc = res.ready() ? (long)nsd_pipe_retarget(res.pipe, lt, mode) : (long)res.create(lt, mode);
+	if (rc != NSD_OK) {
 		nsd_pcap_close(p);
-		return NSD_ERR_HIP;
+		return rc;
 	}
+	nsd_pipe *const pipe = res.pipe;
 	struct Slot {
 		uint8_t *frames = nullptr;
 		nsd_desc_t *desc = nullptr;
@@ -424,21 +483,18 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		long prc = NSD_OK;         // first render error
 	};
 	std::vector<Slot> b(NSLOT);
-	long rc = NSD_OK;
-	for (auto &x : b) {
-		x.frames = (uint8_t *)nsd_host_alloc(FRAME_BYTES);
-		x.desc = (nsd_desc_t *)nsd_host_alloc(BATCH * sizeof(nsd_desc_t));
-		x.rec = (nsd_crec *)nsd_host_alloc(BATCH * sizeof(nsd_crec));
-		x.ext = (uint32_t *)nsd_host_alloc(ext_words * sizeof(uint32_t));
-		x.verdict = (uint32_t *)malloc(BATCH * sizeof(uint32_t));
-		if (has_ll)
-			x.sll = (nsd_sll_t *)nsd_host_alloc(BATCH * sizeof(nsd_sll_t));
-		if (pcap_fd >= 0)
-			x.rhdr = (uint8_t *)malloc((size_t)BATCH * 32);
+	std::vector<uint32_t> verdicts(filter ? (size_t)NSLOT * BATCH : 0);
+	std::vector<uint8_t> rhdrs(pcap_fd >= 0 ? (size_t)NSLOT * BATCH * 32 : 0);
+	for (int k = 0; k < NSLOT; k++) {
+		Slot &x = b[k];
+		x.frames = res.buf[k].frames;
+		x.desc = res.buf[k].desc;
+		x.rec = res.buf[k].rec;
+		x.ext = res.buf[k].ext;
+		x.sll = has_ll ? res.buf[k].sll : nullptr;
+		x.verdict = filter ? &verdicts[(size_t)k * BATCH] : nullptr;
+		x.rhdr = pcap_fd >= 0 ? &rhdrs[(size_t)k * BATCH * 32] : nullptr;
 		x.part.resize(threads);
-		if (!x.frames || !x.desc || !x.rec || !x.ext || !x.verdict || (has_ll && !x.sll) ||
-		    (pcap_fd >= 0 && !x.rhdr))
-			rc = NSD_ERR_NOMEM;
 	}
 
 	std::mutex mu;
@@ -750,18 +806,18 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	for (auto &t : pool)
 		t.join();
 	writer.join();
-	for (auto &x : b) {
-		nsd_host_free(x.frames);
-		nsd_host_free(x.desc);
-		nsd_host_free(x.sll);
-		free(x.rhdr);
-		nsd_host_free(x.rec);
-		nsd_host_free(x.ext);
-		free(x.verdict);
-	}
-	nsd_pipe_destroy(pipe);
+	// (an error leaves batches in the pipe: drop the cached set then)
+	if (&res == &own || rc != NSD_OK)
+		res.release();
 	nsd_pcap_close(p);
 	return rc == NSD_OK ? printed : rc;
+}
+
+// dissector_cleanup_all (nsd_proto.cpp) frees the replay's cached buffers
+extern "C" __attribute__((visibility("hidden"))) void nsd_replay_release(void)
+{
+	std::lock_guard<std::mutex> g(g_replay_mu);
+	g_replay.release();
 }
 
 // ---- TPACKET_V3 ring front end (walk_t3_block, netsniff-ng.c:990-1039) ------

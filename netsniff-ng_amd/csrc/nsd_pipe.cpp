@@ -157,8 +157,10 @@ static int complete_oldest(nsd_pipe *p)
 		if (s.ext_count_out)
 			*s.ext_count_out = used;
 		// compact records: the side words [0, n) and the entries after them,
-		// only when a record of the batch needs either
-		const uint64_t need = p->compact ? (s.small_h[8 + NSD_CNT_EXT] ? (uint64_t)s.n + used : 0) : used;
+		// only when a record of the batch needs either (a chain in the ext
+		// form, or a host-rendered leaf's end)
+		const bool side = s.small_h[8 + NSD_CNT_EXT] || s.small_h[8 + NSD_CNT_HOST];
+		const uint64_t need = p->compact ? (side ? (uint64_t)s.n + used : 0) : used;
 		const uint32_t k = need < p->ext_cap ? (uint32_t)need : p->ext_cap;
 		if (k && s.ext_out &&
 		    !ok(hipMemcpyAsync(s.ext_out, s.ext, (size_t)k * 4, hipMemcpyDeviceToHost,
@@ -279,6 +281,17 @@ static int pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len, co
 	if (!good)
 		s.status = NSD_ERR_HIP;
 	return good ? NSD_OK : NSD_ERR_HIP;
+}
+
+// point an idle pipe at another link type / print mode (the pcap replay keeps
+// one pipe for the process, nsd_pcap.cpp)
+extern "C" __attribute__((visibility("hidden"))) int nsd_pipe_retarget(nsd_pipe *p, int linktype, int mode)
+{
+	if (!p || p->count || mode < PRINT_NORM || mode > PRINT_NONE)
+		return NSD_ERR_ARG;
+	p->start_id = nsd_start_for(linktype);
+	p->mode = mode;
+	return NSD_OK;
 }
 
 extern "C" void *nsd_host_alloc(size_t len)

@@ -196,16 +196,18 @@ def lib():
                                                  _vp, _vp]
         L.nsd_format_batch_compact.restype = ctypes.c_long
         L.nsd_format_batch_compact.argtypes = [_vp, _vp, _vp, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]
-        L.nsd_pipe_create_compact.restype = _vp
-        L.nsd_pipe_create_compact.argtypes = [_u32, _sz, _u32, _int, _int, _int]
-        L.nsd_pipe_submit_compact.restype = _int
-        L.nsd_pipe_submit_compact.argtypes = [_vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]
-        L.nsd_format_range_compact.restype = ctypes.c_long
-        L.nsd_format_range_compact.argtypes = [_vp, _vp, _vp, _u32, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp,
-                                               _vp]
-        L.nsd_set_schedule.restype = _int
-        L.nsd_set_schedule.argtypes = [_int]
-        L.nsd_last_schedule.restype = _int
+        # (entries newer than a dev tool's variant library may lack: bound when
+        # present, tests/test_abi.py checks the product library has them all)
+        for name, res, args in (
+                ("nsd_pipe_create_compact", _vp, [_u32, _sz, _u32, _int, _int, _int]),
+                ("nsd_pipe_submit_compact", _int, [_vp, _vp, _sz, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+                ("nsd_format_range_compact", ctypes.c_long,
+                 [_vp, _vp, _vp, _u32, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]),
+                ("nsd_set_schedule", _int, [_int]),
+                ("nsd_last_schedule", _int, [])):
+            if hasattr(L, name):
+                getattr(L, name).restype = res
+                getattr(L, name).argtypes = args
         L.nsd_replay_pcap.restype = ctypes.c_long
         L.nsd_replay_pcap.argtypes = [ctypes.c_char_p, _int, _vp, _int, _int, _vp, _int]
         _lib = L
@@ -220,6 +222,8 @@ def set_schedule(sched):
     """Force the batch walks' kernel schedule (SCHED_SPLIT / SCHED_FUSED) or
     let the library pick it (SCHED_ADAPTIVE, the default); returns the
     previous setting."""
+    if not hasattr(lib(), "nsd_set_schedule"):
+        return 0   # (a dev tool's variant library from before schedules)
     rc = lib().nsd_set_schedule(sched)
     if rc < 0:
         raise ValueError(f"bad schedule {sched}")
@@ -227,8 +231,9 @@ def set_schedule(sched):
 
 
 def last_schedule():
-    """"split" / "fused": the schedule of the last launch (None before any)."""
-    return SCHED_NAMES.get(lib().nsd_last_schedule())
+    """"split" / "fused": the schedule of the last launch (None before any,
+    or from a library without schedules)."""
+    return SCHED_NAMES.get(lib().nsd_last_schedule()) if hasattr(lib(), "nsd_last_schedule") else None
 
 
 class NsdError(RuntimeError):

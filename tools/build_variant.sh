@@ -6,13 +6,19 @@
 # sources, never switches in the product sources.
 #   tools/build_variant.sh u8 -DNSD_CSUM_U=8
 #   PATCH=/tmp/nop2.patch tools/build_variant.sh nop2
+#   REV=HEAD~1 tools/build_variant.sh prev        (a committed revision's kernels)
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
 d=variants/$name
 rm -rf $d && mkdir -p $d/x/a $d/x/include
-cp -r netsniff-ng_amd/csrc $d/x/a/csrc
-cp include/netsniff_dissect.h $d/x/include/
+if [ -n "$REV" ]; then   # the sources of a git revision instead of the working tree
+  mkdir -p $d/x/a/csrc && git archive "$REV" netsniff-ng_amd/csrc | tar -x -C $d/x/a --strip-components=1
+  git show "$REV":include/netsniff_dissect.h > $d/x/include/netsniff_dissect.h
+else
+  cp -r netsniff-ng_amd/csrc $d/x/a/csrc
+fi
+[ -n "$REV" ] || cp include/netsniff_dissect.h $d/x/include/
 if [ -n "$PATCH" ]; then patch -s -d $d/x/a -p0 < "$PATCH"; fi
 make -s -C netsniff-ng_amd
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function $*"

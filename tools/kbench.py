@@ -27,13 +27,16 @@ def main():
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--records", default="both", choices=["compact", "full", "both"])
+    ap.add_argument("--sched", default="adaptive", choices=["adaptive", "split", "fused"],
+                    help="kernel schedule (nsd_set_schedule)")
     ap.add_argument("--lib", default=None, help="a variant libnsdissect.so (tools/build_variant.sh) "
                     "loaded instead of the in-tree one (dev tools only; the product loads its own)")
     args = ap.parse_args()
     import nsd
     if args.lib:
         nsd.LIB_PATH = os.path.abspath(args.lib)
-    print(f"library {os.path.relpath(nsd.LIB_PATH, ROOT)}", flush=True)
+    print(f"library {os.path.relpath(nsd.LIB_PATH, ROOT)} schedule {args.sched}", flush=True)
+    nsd.set_schedule({"adaptive": nsd.SCHED_ADAPTIVE, "split": nsd.SCHED_SPLIT, "fused": nsd.SCHED_FUSED}[args.sched])
     import bench
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -44,7 +47,7 @@ def main():
             ms = bench.time_steps(b, args.mode, args.steps, args.warmup, 0 if compact else args.grid)
             cnt = b.counters.cpu().numpy().view(np.uint64)
             r = b.roofline(ms)
-            print(f"{key:6s} rec{b.rec_b:<2d} kernel_ms={ms:.4f} frac={r['frac'] if r else None} "
+            print(f"{key:6s} rec{b.rec_b:<2d} {nsd.last_schedule()} kernel_ms={ms:.4f} frac={r['frac'] if r else None} "
                   f"read_frac={r['read_frac'] if r else None} pkts_counted={int(cnt[32])}", flush=True)
             if os.environ.get("KB_PHASES"):
                 # counters 48..55 of an instrumented variant (tools/variants/phases.patch),
