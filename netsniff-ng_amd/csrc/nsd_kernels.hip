@@ -192,7 +192,26 @@ struct LSrc {
 	{
 		uint32_t sum = 0;
 		const uint32_t r = o + m - wb;
-		if (!(r & 1) && in_window(o, 2 * nwords) && (FAST || o + 2 * nwords <= caplen)) {
+		if (FAST && !(r & 1)) {
+			// the fast walk sums only inside the window (its callers check
+			// in_window).  Even start: a leading half, whole dwords four
+			// reads at a time (independent LDS reads, one wait per four:
+			// an IPv4 header of 20 bytes is one round), a trailing half.
+			// Reads past the count are selected away (they stay in LDS).
+			uint32_t j = r >> 2, k = nwords;
+			if ((r & 2) && k) { sum += dw(j) >> 16; j++; k--; }
+			const uint32_t nd = k >> 1;
+			for (uint32_t t = 0; t < nd; t += 4) {
+				const uint32_t v0 = dw(j + t), v1 = dw(j + t + 1), v2 = dw(j + t + 2), v3 = dw(j + t + 3);
+				sum = __builtin_amdgcn_sad_u16(v0, 0u, sum);
+				sum = __builtin_amdgcn_sad_u16(t + 1 < nd ? v1 : 0u, 0u, sum);
+				sum = __builtin_amdgcn_sad_u16(t + 2 < nd ? v2 : 0u, 0u, sum);
+				sum = __builtin_amdgcn_sad_u16(t + 3 < nd ? v3 : 0u, 0u, sum);
+			}
+			if (k & 1) sum += dw(j + nd) & 0xFFFF;
+			return sum;
+		}
+		if (!(r & 1) && in_window(o, 2 * nwords) && o + 2 * nwords <= caplen) {
 			uint32_t j = r >> 2, k = nwords;
 			if ((r & 2) && k) { sum += dw(j) >> 16; j++; k--; }
 			for (; k >= 2; k -= 2, j++)
@@ -1830,6 +1849,10 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 		return 0;   // no chains: nothing deferred
 	uint32_t wcap = grid > 0 ? (uint32_t)grid
 				 : (uint32_t)(s_cus * occupancy((const void *)walk[ci][mi], s_wocc[ci][mi], 4));
+#ifdef NSD_WALK_GRID_CAP
+	if (wcap > NSD_WALK_GRID_CAP)
+		wcap = NSD_WALK_GRID_CAP;
+#endif
 	const uint32_t wblocks = fblocks < wcap ? fblocks : wcap;
 	const uint32_t per_wave = (nlists + wblocks * WAVES - 1) / (wblocks * WAVES);   // lists per walker wave
 	hipLaunchKernelGGL(walk[ci][mi], dim3(wblocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, d_rec, d_ext,
