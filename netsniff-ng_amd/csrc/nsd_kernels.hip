@@ -211,6 +211,21 @@ struct LSrc {
 			if (k & 1) sum += dw(j + nd) & 0xFFFF;
 			return sum;
 		}
+		if (FAST) {
+			// odd start (frames at odd offsets): the dword at window position
+			// r, funnel-shifted out of two row dwords, holds the words at o
+			// and o + 2; two per round, then a trailing word
+			const uint32_t j = r >> 2, sh = r & 3, nd = nwords >> 1;
+			for (uint32_t t = 0; t < nd; t += 2) {
+				const uint32_t v0 = dw(j + t), v1 = dw(j + t + 1), v2 = dw(j + t + 2);
+				sum = __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(v1, v0, sh), 0u, sum);
+				sum = __builtin_amdgcn_sad_u16(t + 1 < nd ? __builtin_amdgcn_alignbyte(v2, v1, sh) : 0u, 0u,
+							       sum);
+			}
+			if (nwords & 1)
+				sum += __builtin_amdgcn_alignbyte(dw(j + nd + 1), dw(j + nd), sh) & 0xFFFF;
+			return sum;
+		}
 		if (!(r & 1) && in_window(o, 2 * nwords) && o + 2 * nwords <= caplen) {
 			uint32_t j = r >> 2, k = nwords;
 			if ((r & 2) && k) { sum += dw(j) >> 16; j++; k--; }
