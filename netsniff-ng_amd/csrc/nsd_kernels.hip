@@ -62,6 +62,11 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #endif
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+// a chunk in global memory: an address rebuilt from shuffled integers is a
+// generic pointer, which compiles to flat_load; flat loads count in lgkmcnt
+// too, so every LDS wait of the walk would also wait for the next tile's
+// chunks.  Loads through this type are global_load.
+typedef __attribute__((address_space(1))) const v4u gv4u;
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m)
 {
 	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -279,7 +284,7 @@ __device__ __forceinline__ void stage_load(Chunks<WIN> &ch, const uint8_t *frame
 			// streaming loads (nt): C2 -9 %, C3 -2 %; C4 +5 % (its general
 			// walk re-reads the first line from HBM rather than L2)
 			const uint64_t src = ((uint64_t)(ahr & 0xFFFFFFu) << 32 | alo) + pos;
-			const v4u t4 = __builtin_nontemporal_load((const v4u *)src);
+			const v4u t4 = __builtin_nontemporal_load((const gv4u *)src);
 			ch.v[r] = make_uint4(t4.x, t4.y, t4.z, t4.w);
 		} else {
 			ch.v[r] = make_uint4(0, 0, 0, 0);
@@ -1844,6 +1849,10 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	// grid > 0 (tests): both kernels' grids capped at `grid` blocks
 	uint32_t fcap = grid > 0 ? (uint32_t)grid
 				 : (uint32_t)(s_cus * occupancy((const void *)fast[ci][mi], s_focc[ci][mi], 8));
+#ifdef NSD_FAST_BPC
+	if (grid <= 0)
+		fcap = (uint32_t)(s_cus * NSD_FAST_BPC);   // experiments: fewer resident blocks than fit
+#endif
 	if (fcap > NSD_MAX_GRID)
 		fcap = NSD_MAX_GRID;
 	const uint32_t fblocks = want < fcap ? want : fcap;
