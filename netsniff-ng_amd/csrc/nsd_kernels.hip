@@ -37,10 +37,11 @@ namespace nsd {
 constexpr int BLOCK = 256;
 constexpr int WAVES = BLOCK / 64;
 
-// Packets the fast walk handed to the general walk, summed over launches on
-// this device: the launcher samples it now and then to choose the schedule
-// (split or fused, nsd_launch_dissect_rec)
-__device__ unsigned long long g_deferred;
+// Summed over launches on this device and sampled now and then by the
+// launcher to choose the schedule (split or fused, nsd_launch_dissect_rec):
+// [0] packets the fast walk handed to the general walk, [1] ICMPv4 messages
+// left to a checksum pass (longer than their window)
+__device__ unsigned long long g_sched_acc[2];
 constexpr int WIN1 = 64;         // bytes per staged window, pass 1
 #ifndef NSD_WIN2
 #define NSD_WIN2 128
@@ -968,7 +969,9 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	}
 	fc.flush(s_cnt, lane);
 	if (lane == 0 && ndefer)
-		atomicAdd(&g_deferred, (unsigned long long)ndefer);
+		atomicAdd(&g_sched_acc[0], (unsigned long long)ndefer);
+	if (lane == 0 && pq.npend)
+		atomicAdd(&g_sched_acc[1], (unsigned long long)pq.npend);
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
@@ -1456,7 +1459,9 @@ __global__ __launch_bounds__(BLOCK, CR ? NSD_FAST_MINW : NSD_FAST_MINW_FULL) voi
 		cnts[gw] = make_uint2(ndef, nicmp);
 		sh.pcnt[wv] = nicmp;
 		if (ndef)
-			atomicAdd(&g_deferred, (unsigned long long)ndef);
+			atomicAdd(&g_sched_acc[0], (unsigned long long)ndef);
+		if (nicmp)
+			atomicAdd(&g_sched_acc[1], (unsigned long long)nicmp);
 	}
 	if (MODE == PRINT_NORM) {
 		__syncthreads();   // records final, the block's pending lists and counts complete
@@ -1630,18 +1635,25 @@ static size_t region_slots(uint32_t n)
 // ---- the schedule -------------------------------------------------------------
 // split (dissect_fast + dissect_walk) or fused (dissect_all).  The split
 // schedule runs the fast walk at 6 waves per SIMD instead of 4 and wins when
-// few packets need the general walk (C2 16M x 64 B: 0.221 against 0.249 ms,
-// C3 equal); when most do (C4's IPv6 extension chains) the fused kernel
-// wins by far (1.17 against 1.88 ms): its walkers take a tile's packets while
-// their first lines are still on chip, where the walker kernel re-reads them
-// and the fast kernel writes a list entry per packet.  Adaptive (the
-// default): every NSD_SCHED_SAMPLE launches on a device the launcher queues a
-// copy of the device's deferral count (g_deferred, the packets the fast walk
-// handed over) to pinned host memory and resets it; once a copy has landed,
-// the share of deferred packets picks the schedule for the launches after
-// it, with hysteresis (fused above 15 %, split again below 5 %).  A capture's
-// traffic mix changes slowly against batches of a few milliseconds; both
-// schedules give identical results.  nsd_set_schedule forces one (tests).
+// the fast walk finishes nearly every packet and few ICMPv4 messages run
+// past their windows (C2 16M x 64 B: 0.233 against 0.249 ms).  When many
+// packets need the general walk (C4's IPv6 extension chains) the fused
+// kernel wins by far (1.17 against 1.88 ms): its walkers take a tile's
+// packets while their first lines are still on chip, where the walker
+// kernel re-reads them and the fast kernel writes a list entry per packet.
+// When many ICMPv4 checksums are left to a pass (C3 IMIX: about a fifth of
+// the packets) the fused kernel wins too (0.70 - 0.75 against 0.73 - 0.81
+// ms on the same boxes, r03): its checksum pass streams at 4 waves per SIMD
+// with 8 loads in flight per lane.  Adaptive (the default): every
+// NSD_SCHED_SAMPLE launches on a device the launcher queues a copy of the
+// device's two sample counts (g_sched_acc: packets the fast walk handed
+// over, ICMPv4 messages left to a pass) to pinned host memory and resets
+// them; once a copy has landed, their shares of the packets pick the
+// schedule for the launches after it, with hysteresis (fused above 15 %
+// deferred or 10 % pending checksums, split again below 5 % of both).  A
+// capture's traffic mix changes slowly against batches of a few
+// milliseconds; both schedules give identical results.  nsd_set_schedule
+// forces one (tests).
 #ifndef NSD_SCHED_SAMPLE
 #define NSD_SCHED_SAMPLE 32
 #endif
@@ -1678,8 +1690,9 @@ bool sched_fused(uint32_t n)
 		fused = g_sched_force == NSD_SCHED_FUSED;
 	} else {
 		if (S.pending && hipEventQuery(S.ev) == hipSuccess) {
-			const double rate = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
-			S.fused = S.fused ? rate > 0.05 : rate > 0.15;
+			const double rd = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
+			const double ri = S.sampled ? (double)S.host[1] / (double)S.sampled : 0.0;
+			S.fused = S.fused ? rd > 0.05 || ri > 0.05 : rd > 0.15 || ri > 0.10;
 			S.pending = false;
 		}
 		fused = S.fused;
@@ -1699,15 +1712,15 @@ void sched_sample(hipStream_t stream)
 		return;
 	if (!S.init) {
 		S.init = true;
-		if (hipHostMalloc((void **)&S.host, 8, hipHostMallocDefault) != hipSuccess ||
-		    hipGetSymbolAddress(&S.dev_acc, HIP_SYMBOL(nsd::g_deferred)) != hipSuccess ||
+		if (hipHostMalloc((void **)&S.host, 16, hipHostMallocDefault) != hipSuccess ||
+		    hipGetSymbolAddress(&S.dev_acc, HIP_SYMBOL(nsd::g_sched_acc)) != hipSuccess ||
 		    hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
 			S.host = nullptr;
 	}
 	if (!S.host)
 		return;
-	if (hipMemcpyAsync(S.host, S.dev_acc, 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-	    hipMemsetAsync(S.dev_acc, 0, 8, stream) != hipSuccess || hipEventRecord(S.ev, stream) != hipSuccess)
+	if (hipMemcpyAsync(S.host, S.dev_acc, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+	    hipMemsetAsync(S.dev_acc, 0, 16, stream) != hipSuccess || hipEventRecord(S.ev, stream) != hipSuccess)
 		return;
 	S.sampled = S.pkts;
 	S.pkts = 0;

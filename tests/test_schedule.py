@@ -1,8 +1,9 @@
 """The adaptive kernel schedule (nsd_launch_dissect_rec):
 with no schedule forced, batches whose packets mostly go to the general
-walk (C4's IPv6 extension chains) switch the launches to the fused kernel,
-batches the fast walk finishes (C2) switch them back to the split kernels,
-and the records stay those of the oracle throughout."""
+walk (C4's IPv6 extension chains) or leave many ICMPv4 checksums to a pass
+(C3 IMIX) switch the launches to the fused kernel, batches the fast walk
+finishes (C2) switch them back to the split kernels, and the records stay
+those of the oracle throughout."""
 import numpy as np
 import pytest
 
@@ -23,13 +24,14 @@ def test_adaptive_schedule_follows_the_traffic():
     prev = nsd.set_schedule(nsd.SCHED_ADAPTIVE)
     try:
         batches = {}
-        for cfg in (T.SYN_IPV6X, T.SYN_UDP64):
+        for cfg in (T.SYN_IPV6X, T.SYN_UDP64, T.SYN_IMIX):
             frames, desc = T.make_batch(cfg, 1 << 16)
             orec, oext, ocnt, _ = T.oracle_records(frames, desc)
             want, _ = nsd.compact_of(orec, oext)
             batches[cfg] = (torch.from_numpy(frames).cuda(), torch.from_numpy(desc.view(np.int64)).cuda(), want,
                             ocnt)
-        for cfg, sched in ((T.SYN_IPV6X, "fused"), (T.SYN_UDP64, "split"), (T.SYN_IPV6X, "fused")):
+        for cfg, sched in ((T.SYN_IPV6X, "fused"), (T.SYN_UDP64, "split"), (T.SYN_IMIX, "fused"),
+                           (T.SYN_UDP64, "split"), (T.SYN_IPV6X, "fused")):
             f, d, want, ocnt = batches[cfg]
             seen = []
             for _ in range(160):
