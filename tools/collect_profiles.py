@@ -7,8 +7,11 @@ profile files:
   profiles/<tag>_bench_c5_one_gpu.json C5's 128M IMIX packets on one GPU
   profiles/<tag>_kernel_stats.csv      rocprofv3 --kernel-trace --stats of the
                                        default bench command (--no-pmc)
-  profiles/<tag>_kernel_check.json     per dissect_all instantiation: rocprof
-                                       average vs the bench's HIP-event time
+  profiles/<tag>_kernel_check.json     per workload: the rocprof trace's kernels
+                                       (fused dissect_all, or split dissect_fast
+                                       + dissect_walk), their averages, the
+                                       launch span and period, against the
+                                       bench's HIP-event time
   profiles/<tag>_pytest_gpu.log, <tag>_smoke.log
 
 The bench's `traffic` comes from its own two rocprofv3 --pmc child passes
@@ -51,7 +54,7 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "round")):
         rows = {}
         with open(st) as f:
             for row in csv.DictReader(f):
-                if "dissect_all" in row["Name"]:
+                if "nsd::dissect_" in row["Name"]:
                     rows[row["Name"]] = {"calls": int(row["Calls"]),
                                          "average_us": float(row["AverageNs"]) / 1e3}
         bench = last_json(os.path.join(src, "stats.log"))
@@ -66,37 +69,63 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "round")):
         if os.path.exists(tr) and bench:
             b = json.loads(bench)
             steps = b["steps"]
-            d = {}
+            # one launch = dissect_all (fused) or dissect_fast + dissect_walk
+            # (split); per record form (the template's bool), in time order
+            launches = {"true": [], "false": []}
             with open(tr) as f:
                 for row in csv.DictReader(f):
-                    if "dissect_all" in row["Kernel_Name"]:
-                        d.setdefault(row["Kernel_Name"].split("(")[0], []).append(
-                            (int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+                    nm = row["Kernel_Name"]
+                    if "nsd::dissect_" not in nm or "<0," not in nm:
+                        continue
+                    kern = nm.split("nsd::")[1].split("<")[0]
+                    form = "true" if "<0, true>" in nm else "false"
+                    launches[form].append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), kern))
 
-            def runs(ds):
-                ds = sorted(ds)
+            def steps_of(ks):
+                out = []
+                for s0, e0, kern in sorted(ks):
+                    if kern == "dissect_walk" and out and out[-1]["kernels"][-1][0] == "dissect_fast":
+                        out[-1]["kernels"].append((kern, s0, e0))
+                        out[-1]["end"] = e0
+                    else:
+                        out.append({"start": s0, "end": e0, "kernels": [(kern, s0, e0)]})
+                return out
+
+            def runs(st):
                 out, cur = [], []
-                for s0, e0 in ds:
-                    if cur and s0 - cur[-1][1] > 50_000_000:
+                for x in st:
+                    if cur and x["start"] - cur[-1]["end"] > 50_000_000:
                         out.append(cur)
                         cur = []
-                    cur.append((s0, e0))
+                    cur.append(x)
                 if cur:
                     out.append(cur)
                 return out
 
-            def avg_us(seg):
-                return round(sum(e0 - s0 for s0, e0 in seg) / len(seg) / 1e3, 1) if seg else None
+            def summary(seg):
+                if not seg:
+                    return None
+                per = {}
+                for x in seg:
+                    for kern, s0, e0 in x["kernels"]:
+                        per.setdefault(kern, []).append((e0 - s0) / 1e3)
+                spans = [(x["end"] - x["start"]) / 1e3 for x in seg]
+                gaps = [(seg[k + 1]["start"] - seg[k]["end"]) / 1e3 for k in range(len(seg) - 1)]
+                return {"schedule": "fused" if "dissect_all" in per else "split",
+                        "kernel_avg_us": {k: round(sum(v) / len(v), 1) for k, v in per.items()},
+                        "launch_span_avg_us": round(sum(spans) / len(spans), 1),
+                        "launch_period_avg_us": round((seg[-1]["end"] - seg[0]["start"]) / 1e3 / len(seg), 1),
+                        "gap_avg_us": round(sum(gaps) / len(gaps), 2) if gaps else None}
 
             names = ["headline"] + list((b.get("legs") or {}).keys())
             split = {}
-            for k, run in enumerate(runs(d.get("void nsd::dissect_all<0, true>", []))):
+            for k, run in enumerate(runs(steps_of(launches["true"]))):
                 if k < len(names):
-                    split[names[k]] = avg_us(run[-steps:] if k == 0 else run[-steps - 1:-1])
-            full = runs(d.get("void nsd::dissect_all<0, false>", []))
+                    split[names[k]] = summary(run[-steps:] if k == 0 else run[-steps - 1:-1])
+            full = runs(steps_of(launches["false"]))
             if full:
-                split["other_records"] = avg_us(full[0][-steps - 1:-1])
-            check["rocprof_trace_avg_us"] = split
+                split["other_records"] = summary(full[0][-steps - 1:-1])
+            check["rocprof_trace"] = split
         if bench:
             b = json.loads(bench)
             check["bench_kernel_ms"] = {"headline": b["roofline"]["kernel_ms"] if b.get("roofline") else None}
