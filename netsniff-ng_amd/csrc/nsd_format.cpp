@@ -21,6 +21,7 @@
 
 #include "../../include/netsniff_dissect.h"
 #include "nsd_lookup.h"
+#include "nsd_ntop.h"
 
 namespace nsd {
 
@@ -120,14 +121,14 @@ static void ntop4(const Frame &f, uint64_t off, char *buf)
 {
 	uint8_t a[4];
 	for (int i = 0; i < 4; i++) a[i] = f.b(off + i);
-	inet_ntop(AF_INET, a, buf, INET_ADDRSTRLEN);
+	ntop4_to(a, buf);   // inet_ntop's text (nsd_ntop.h)
 }
 
 static void ntop6(const Frame &f, uint64_t off, char *buf)
 {
 	uint8_t a[16];
 	for (int i = 0; i < 16; i++) a[i] = f.b(off + i);
-	inet_ntop(AF_INET6, a, buf, INET6_ADDRSTRLEN);
+	ntop6_to(a, buf);
 }
 
 // ether_lookup_addr (proto_ethernet.c:33-46)
@@ -655,7 +656,7 @@ static Done r_mobility(Out &o, const Frame &f, const Layer &L, int mode)
 			uint64_t v = f.be64(at + 2);
 			memcpy(a, &v, 8);
 			char buf[INET6_ADDRSTRLEN];
-			inet_ntop(AF_INET6, a, buf, sizeof(buf));
+			ntop6_to(a, buf);
 			o << "Status (0x";
 			o.x(f.b(at)) << ") Home Addr (" << buf << ")";
 			opts();
@@ -1237,8 +1238,12 @@ extern "C" long nsd_format_range_compact(const uint8_t *frames, const nsd_desc_t
 {
 	if (hi < lo || (hi > lo && (!frames || !desc || !crec)))
 		return NSD_ERR_ARG;
-	std::string s;
-	s.reserve(cap ? cap : 4096);
+	// a per-thread buffer that keeps its capacity across calls (reserving
+	// `cap` per call faulted in fresh pages every time: threads formatting
+	// ranges in parallel then queued on the process's page-table lock)
+	static thread_local std::string t_buf;
+	std::string &s = t_buf;
+	s.clear();
 	for (uint32_t i = lo; i < hi; i++) {
 		const uint64_t d = desc[i];
 		int r = nsd::format_packet_compact(s, frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), linktype, mode,
