@@ -380,6 +380,10 @@ struct ReplayRes {
 		nsd_crec *rec;
 		uint32_t *ext;
 	} buf[NSLOT] = {};
+	// the formatter parts' text buffers per slot, kept with their capacity:
+	// regrown per replay they faulted in hundreds of MB of fresh pages,
+	// with the formatter threads queued on the page-table lock
+	std::vector<std::string> part[NSLOT];
 	bool ready() const { return pipe != nullptr; }
 	long create(int lt, int mode)
 	{
@@ -409,6 +413,8 @@ struct ReplayRes {
 			nsd_host_free(x.ext);
 			x = {};
 		}
+		for (auto &v : part)
+			std::vector<std::string>().swap(v);
 		nsd_pipe_destroy(pipe);
 		pipe = nullptr;
 	}
@@ -479,7 +485,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		int status = 0;
 		uint64_t seq = 0;
 		int parts = 0, left = 0;   // render jobs, jobs not done
-		std::vector<std::string> part;
+		std::vector<std::string> *part = nullptr;   // res.part[slot]
 		long prc = NSD_OK;         // first render error
 	};
 	std::vector<Slot> b(NSLOT);
@@ -494,7 +500,9 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		x.sll = has_ll ? res.buf[k].sll : nullptr;
 		x.verdict = filter ? &verdicts[(size_t)k * BATCH] : nullptr;
 		x.rhdr = pcap_fd >= 0 ? &rhdrs[(size_t)k * BATCH * 32] : nullptr;
-		x.part.resize(threads);
+		x.part = &res.part[k];
+		if (x.part->size() < (size_t)threads)
+			x.part->resize(threads);
 	}
 
 	std::mutex mu;
@@ -525,7 +533,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	auto put_parts = [&](const Slot &x) -> long {
 		if (cols > 0) {
 			for (int t = 0; t < x.parts; t++) {
-				const long r = put_text(x.part[t]);
+				const long r = put_text((*x.part)[t]);
 				if (r != NSD_OK)
 					return r;
 			}
@@ -533,8 +541,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		}
 		std::vector<struct iovec> iov;
 		for (int t = 0; t < x.parts; t++)
-			if (!x.part[t].empty())
-				iov.push_back({ (void *)x.part[t].data(), x.part[t].size() });
+			if (!(*x.part)[t].empty())
+				iov.push_back({ (void *)(*x.part)[t].data(), (*x.part)[t].size() });
 		size_t k = 0;
 		while (k < iov.size()) {
 			const int cnt = (int)(iov.size() - k < 512 ? iov.size() - k : 512);
@@ -570,7 +578,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	// formatter pool: part t of a slot = its packets [n t / parts, n (t+1) / parts)
 	auto render = [&](Slot &x, int t) -> long {
 		const uint32_t lo = (uint32_t)((uint64_t)x.n * t / x.parts), hi = (uint32_t)((uint64_t)x.n * (t + 1) / x.parts);
-		std::string &s = x.part[t];
+		std::string &s = (*x.part)[t];
 		s.clear();
 		for (uint32_t k = lo; k < hi; k++) {
 			const uint64_t d = x.desc[k];
