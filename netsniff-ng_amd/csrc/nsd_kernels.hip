@@ -266,7 +266,11 @@ struct Chunks {
 // them to the loading lanes (the end, capped at 255 - the window is shorter
 // - rides in the address's high dword, a 48-bit VA leaves its top byte
 // free).  The count of valid bytes per chunk is kept for stage_write.
-template <int WIN>
+// ALL (the split fast loop): every chunk load is issued, chunks wholly past
+// caplen too (stage_write zeroes them; a 64-byte window always lies inside
+// the frame buffer's NSD_FRAME_PAD): a load under a branch leaves hipcc
+// unsure whether it is pending, and it then waits vmcnt(0) for the chunks.
+template <int WIN, bool ALL = false>
 __device__ __forceinline__ void stage_load(Chunks<WIN> &ch, const uint8_t *frames, uint64_t my_desc, int lane)
 {
 	constexpr int CPP = Chunks<WIN>::CPP;
@@ -281,7 +285,7 @@ __device__ __forceinline__ void stage_load(Chunks<WIN> &ch, const uint8_t *frame
 		const uint32_t alo = __shfl((uint32_t)a, q, 64), ahr = __shfl(hr, q, 64);
 		const uint32_t pos = 16u * c, qlim = ahr >> 24;
 		const uint32_t nv = qlim > pos ? min(qlim - pos, 16u) : 0u;
-		if (nv) {
+		if (ALL || nv) {
 			// streaming loads (nt): C2 -9 %, C3 -2 %; C4 +5 % (its general
 			// walk re-reads the first line from HBM rather than L2)
 			const uint64_t src = ((uint64_t)(ahr & 0xFFFFFFu) << 32 | alo) + pos;
@@ -448,6 +452,60 @@ __device__ __forceinline__ void put_rec(void *rec, uint32_t i, const WalkOut &w)
 		__builtin_nontemporal_store(v, (v2u *)rec + i);
 	} else {
 		store_rec((uint4 *)rec, i, pack_record(w));
+	}
+}
+
+// The split fast loop's stores.  With NSD_FAST_ASMST they are inline-asm
+// vector stores: hipcc's waitcnt pass treats the vector-memory counter as
+// out of order while loads and stores are both pending and then waits
+// vmcnt(0) for a tile's chunks - for every later chunk load and every store
+// too, which defeats a deeper prefetch.  It does not see these stores, so its
+// waits count the loop's loads alone; loads complete in order among
+// themselves, so a wait that leaves N later loads outstanding still covers
+// the load it waits for, whatever the stores do.  Their completion is ours:
+// drain_stores() before anything reads what they wrote.
+#ifndef NSD_FAST_ASMST
+#define NSD_FAST_ASMST 0
+#endif
+#ifndef NSD_FAST_DEPTH
+#define NSD_FAST_DEPTH 1
+#endif
+__device__ __forceinline__ void st_b32(uint32_t *p, uint32_t v)
+{
+	if (NSD_FAST_ASMST)
+		asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(v) : "memory");
+	else
+		*p = v;
+}
+__device__ __forceinline__ void st_b128(uint4 *p, uint4 x)
+{
+	if (NSD_FAST_ASMST) {
+		const v4u v = { x.x, x.y, x.z, x.w };
+		asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+	} else {
+		*p = x;
+	}
+}
+__device__ __forceinline__ void drain_stores()
+{
+	if (NSD_FAST_ASMST)
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+template <bool CR>
+__device__ __forceinline__ void put_rec_st(void *rec, uint32_t i, const WalkOut &w)
+{
+	if (!NSD_FAST_ASMST) {
+		put_rec<CR>(rec, i, w);
+	} else if constexpr (CR) {
+		const bool more = w.n > NSD_REC_MAX_LAYERS;
+		const uint32_t nf = (more ? NSD_N_EXT : w.n) | w.flags;
+		const uint32_t rs = more && !w.ext_on ? w.n : 0u;
+		const v2u v = { w.ext_on ? w.slot : w.chain, w.ip_csum | nf << 16 | rs << 24 };
+		asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"((v2u *)rec + i), "v"(v) : "memory");
+	} else {
+		const uint4 r = pack_record(w);
+		const v4u v = { r.x, r.y, r.z, r.w };
+		asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"((uint4 *)rec + i), "v"(v) : "memory");
 	}
 }
 
@@ -1164,9 +1222,6 @@ constexpr int FROW = WIN1 / 4;   // fast rows: 16 dwords, 16-byte slots XOR-swiz
 #ifndef NSD_FAST_MINW_FULL
 #define NSD_FAST_MINW_FULL 5     // the same for 16-byte records (the deferral entries carry layer starts)
 #endif
-#ifndef NSD_FAST_PREF
-#define NSD_FAST_PREF 2          // where the next tile's chunk loads are issued (fast_tiles)
-#endif
 #ifndef NSD_FAST_CSUM_U
 #define NSD_FAST_CSUM_U 4        // interior chunk loads in flight per lane (fast_icmp_pass)
 #endif
@@ -1247,14 +1302,24 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 	}
 	if (base >= n)
 		return;
-	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
-	// descriptors are in flight
-	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
-	uint64_t d1 = (base + stride < n && base + stride + lane < n) ? desc[base + stride + lane] : 0;
-	Chunks<WIN1> ch;
-	stage_load<WIN1>(ch, frames, d0, lane);
 	uint32_t *const rows = &sh.win[wv][0];
-	for (; base < n; base += stride) {
+	// Descriptors (a lane past the batch: 0).  With a deeper prefetch they
+	// are loaded unconditionally, from a clamped index (a load under a branch
+	// leaves hipcc unsure whether it is pending, and it then waits vmcnt(0)
+	// for the chunks, i.e. for every load in flight); a lane past the batch
+	// then keeps the last packet's descriptor: it only stages that frame's
+	// window, it walks nothing (valid is false) and counts nothing.
+	// NSD_FAST_DEPTH 2 / 3 (with NSD_FAST_ASMST and 3 blocks per CU) are
+	// experiments, not the product build: DESIGN.md §7.
+	auto dsc = [&](uint32_t b) -> uint64_t {
+		if (NSD_FAST_DEPTH == 1)
+			return b < n && b + lane < n ? desc[b + lane] : 0;
+		return desc[b < n && b + lane < n ? b + lane : n - 1];
+	};
+	// One tile at `base` whose chunks are in `ch` (descriptors d0): write them
+	// to the rows, reuse `ch` for the chunks of the tile NSD_FAST_DEPTH
+	// strides on (descriptors dpre), walk the tile.
+	auto tile = [&](Chunks<WIN1> &ch, const uint64_t d0, const uint64_t dpre) {
 		const uint32_t i = base + lane;
 		const bool valid = i < n;
 		const uint64_t off = NSD_DESC_OFF(d0);
@@ -1262,13 +1327,15 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 		WalkOut w;
 		walk_init(w, caplen, valid ? start_id : 0);
 		stage_write_sw(rows, ch, lane);
-		const uint32_t b2 = base + 2 * stride;
-		const uint64_t d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
-		// the next tile's chunk loads: before this tile's walk (in flight
-		// during it; its registers live across the walk), after the walk, or
-		// after the whole tile (NSD_FAST_PREF 2 / 1 / 0)
-		if (NSD_FAST_PREF == 2 && base + stride < n)
-			stage_load<WIN1>(ch, frames, d1, lane);
+		// (deeper prefetch: issued past the batch's last tile too, from the
+		// clamped descriptor - loads skipped on some paths also make hipcc
+		// wait vmcnt(0))
+		if (NSD_FAST_DEPTH == 1) {
+			if (base + stride < n)
+				stage_load<WIN1>(ch, frames, dpre, lane);
+		} else {
+			stage_load<WIN1, true>(ch, frames, dpre, lane);
+		}
 		wave_sync_lds();
 		uint32_t fw = FW_DONE;
 		if (valid) {
@@ -1278,8 +1345,6 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 		}
 		const bool deferred = fw != FW_DONE;
 		wave_sync_lds();
-		if (NSD_FAST_PREF == 1 && base + stride < n)
-			stage_load<WIN1>(ch, frames, d1, lane);
 		const bool done = valid && !deferred;
 		if (MODE == PRINT_NORM) {
 			// ICMPv4 messages past the window, from the back of the list
@@ -1288,8 +1353,8 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 			if (pnd) {
 				const uint32_t part = fold_weighted(w.icmp_sum, ((uint32_t)off + w.icmp_off) & 1);
 				uint4 *e = list + (size_t)(cap - 1 - (nicmp + lanes_below(pm))) * SW;
-				e[0] = make_uint4(i, w.icmp_off | w.icmp_len << 16, part, 0);
-				e[1] = make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), 0, 0);
+				st_b128(e, make_uint4(i, w.icmp_off | w.icmp_len << 16, part, 0));
+				st_b128(e + 1, make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), 0, 0));
 			}
 			nicmp += (uint32_t)__popcll(pm);
 		}
@@ -1321,11 +1386,11 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 		}
 		if (CR && side && done && (w.flags & NSD_F_HOST)) {
 			// a leaf the fast walk finished (ARP, DCCP): its end in the side word
-			side[i] = w.data;
+			st_b32(side + i, w.data);
 			w.flags |= NSD_F_LEAF_END;
 		}
 		if (done)
-			put_rec<CR>(rec, i, w);
+			put_rec_st<CR>(rec, i, w);
 		fc.add(w, caplen, done);
 		// the deferred packets' walk state, for dissect_walk: from the start
 		// (FW_RESTART; the SLL head is run here) or where the fast walk stopped
@@ -1352,21 +1417,95 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 				// head, Ethernet, 2 tags and IP, layer 0 at 0 and the others
 				// inside the 64-byte window)
 				uint4 *e = list + (size_t)(ndef + lanes_below(dm)) * SW;
-				e[0] = make_uint4(i, w.data | w.tail << 16,
-						  (uint32_t)w.ip_csum | (uint32_t)w.flags << 16 | w.n << 24 | (uint32_t)w.id << 27,
-						  w.chain);
+				st_b128(e, make_uint4(i, w.data | w.tail << 16,
+						      (uint32_t)w.ip_csum | (uint32_t)w.flags << 16 | w.n << 24 |
+							      (uint32_t)w.id << 27,
+						      w.chain));
 				const uint32_t offs = CR ? 0u
 							 : ((uint32_t)(w.offA >> 16) & 0xFF) | ((uint32_t)(w.offA >> 32) & 0xFF) << 8 |
 								   ((uint32_t)(w.offA >> 48) & 0xFF) << 16 | (w.offB & 0xFF) << 24;
-				e[1] = make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), offs, 0);
+				st_b128(e + 1, make_uint4((uint32_t)d0, (uint32_t)(d0 >> 32), offs, 0));
 			}
 			ndef += (uint32_t)__popcll(dm);
 		}
-		if (NSD_FAST_PREF == 0 && base + stride < n)
-			stage_load<WIN1>(ch, frames, d1, lane);
+	};
+#if NSD_FAST_DEPTH == 1
+	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
+	// descriptors are in flight
+	uint64_t d0 = dsc(base), d1 = dsc(base + stride);
+	Chunks<WIN1> ch;
+	stage_load<WIN1>(ch, frames, d0, lane);
+	for (; base < n; base += stride) {
+		const uint64_t d2 = dsc(base + 2 * stride);
+		tile(ch, d0, d1);
 		d0 = d1;
 		d1 = d2;
 	}
+#elif NSD_FAST_DEPTH == 3
+	// three tiles' chunks in flight while one is walked: three register sets
+	// in turn (the loop unrolled by three), descriptors four tiles ahead
+	uint64_t d0 = dsc(base), d1 = dsc(base + stride), d2 = dsc(base + 2 * stride), d3 = dsc(base + 3 * stride);
+	Chunks<WIN1> chA, chB, chC;
+	stage_load<WIN1, true>(chA, frames, d0, lane);
+	stage_load<WIN1, true>(chB, frames, d1, lane);
+	stage_load<WIN1, true>(chC, frames, d2, lane);
+	for (;;) {
+		uint64_t d4 = dsc(base + 4 * stride);
+		tile(chA, d0, d3);
+		d0 = d1;
+		d1 = d2;
+		d2 = d3;
+		d3 = d4;
+		base += stride;
+		if (base >= n)
+			break;
+		d4 = dsc(base + 4 * stride);
+		tile(chB, d0, d3);
+		d0 = d1;
+		d1 = d2;
+		d2 = d3;
+		d3 = d4;
+		base += stride;
+		if (base >= n)
+			break;
+		d4 = dsc(base + 4 * stride);
+		tile(chC, d0, d3);
+		d0 = d1;
+		d1 = d2;
+		d2 = d3;
+		d3 = d4;
+		base += stride;
+		if (base >= n)
+			break;
+	}
+#else
+	// two tiles' chunks in flight while one is walked: two register sets that
+	// swap roles (the loop unrolled by two), descriptors three tiles ahead
+	static_assert(NSD_FAST_DEPTH == 2, "prefetch depth 1, 2 or 3");
+	uint64_t d0 = dsc(base), d1 = dsc(base + stride), d2 = dsc(base + 2 * stride);
+	Chunks<WIN1> chA, chB;
+	stage_load<WIN1, true>(chA, frames, d0, lane);
+	stage_load<WIN1, true>(chB, frames, d1, lane);
+	for (;;) {
+		uint64_t d3 = dsc(base + 3 * stride);
+		tile(chA, d0, d2);
+		d0 = d1;
+		d1 = d2;
+		d2 = d3;
+		base += stride;
+		if (base >= n)
+			break;
+		d3 = dsc(base + 3 * stride);
+		tile(chB, d0, d2);
+		d0 = d1;
+		d1 = d2;
+		d2 = d3;
+		base += stride;
+		if (base >= n)
+			break;
+	}
+#endif
+	drain_stores();   // the loop's records, list entries and side words are complete
 	fc.flush(sh.cnt, lane);
 }
 
