@@ -463,12 +463,17 @@ __device__ __forceinline__ void put_rec(void *rec, uint32_t i, const WalkOut &w)
 // waits count the loop's loads alone; loads complete in order among
 // themselves, so a wait that leaves N later loads outstanding still covers
 // the load it waits for, whatever the stores do.  Their completion is ours:
-// drain_stores() before anything reads what they wrote.
-#ifndef NSD_FAST_ASMST
-#define NSD_FAST_ASMST 0
-#endif
+// drain_stores() before anything reads what they wrote.  A store of more
+// than 8 bytes reads its data registers over two cycles, and hipcc's hazard
+// recognizer does not know an asm statement is such a store: the next VALU
+// could overwrite the data before it is read (gfx9's 12-dword store hazard;
+// without the wait state a depth-3 build wrote corrupt list entries and
+// faulted the GPU).  The 16-byte forms end in s_nop 1.
 #ifndef NSD_FAST_DEPTH
-#define NSD_FAST_DEPTH 1
+#define NSD_FAST_DEPTH 2           // tiles of chunks in flight per fast wave (1..3)
+#endif
+#ifndef NSD_FAST_ASMST
+#define NSD_FAST_ASMST (NSD_FAST_DEPTH > 1)
 #endif
 __device__ __forceinline__ void st_b32(uint32_t *p, uint32_t v)
 {
@@ -481,7 +486,7 @@ __device__ __forceinline__ void st_b128(uint4 *p, uint4 x)
 {
 	if (NSD_FAST_ASMST) {
 		const v4u v = { x.x, x.y, x.z, x.w };
-		asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+		asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 	} else {
 		*p = x;
 	}
@@ -505,7 +510,7 @@ __device__ __forceinline__ void put_rec_st(void *rec, uint32_t i, const WalkOut 
 	} else {
 		const uint4 r = pack_record(w);
 		const v4u v = { r.x, r.y, r.z, r.w };
-		asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"((uint4 *)rec + i), "v"(v) : "memory");
+		asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"((uint4 *)rec + i), "v"(v) : "memory");
 	}
 }
 
@@ -1217,10 +1222,13 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 
 constexpr int FROW = WIN1 / 4;   // fast rows: 16 dwords, 16-byte slots XOR-swizzled by swz_of(q, 4)
 #ifndef NSD_FAST_MINW
-#define NSD_FAST_MINW 6          // waves per SIMD dissect_fast is register-allocated for (compact records)
+#define NSD_FAST_MINW (NSD_FAST_DEPTH > 1 ? 4 : 6)   // waves per SIMD dissect_fast is register-allocated for (compact records)
 #endif
 #ifndef NSD_FAST_MINW_FULL
-#define NSD_FAST_MINW_FULL 5     // the same for 16-byte records (the deferral entries carry layer starts)
+#define NSD_FAST_MINW_FULL (NSD_FAST_DEPTH > 1 ? 4 : 5)   // the same for 16-byte records (the deferral entries carry layer starts)
+#endif
+#ifndef NSD_FAST_BPC
+#define NSD_FAST_BPC (NSD_FAST_DEPTH > 1 ? 3 : 0)   // resident fast blocks per CU (0: as many as fit)
 #endif
 #ifndef NSD_FAST_CSUM_U
 #define NSD_FAST_CSUM_U 4        // interior chunk loads in flight per lane (fast_icmp_pass)
@@ -1309,8 +1317,7 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 	// for the chunks, i.e. for every load in flight); a lane past the batch
 	// then keeps the last packet's descriptor: it only stages that frame's
 	// window, it walks nothing (valid is false) and counts nothing.
-	// NSD_FAST_DEPTH 2 / 3 (with NSD_FAST_ASMST and 3 blocks per CU) are
-	// experiments, not the product build: DESIGN.md §7.
+	// The product build runs depth 2 (inline-asm stores, 3 blocks per CU).
 	auto dsc = [&](uint32_t b) -> uint64_t {
 		if (NSD_FAST_DEPTH == 1)
 			return b < n && b + lane < n ? desc[b + lane] : 0;
@@ -2001,10 +2008,10 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	// grid > 0 (tests): both kernels' grids capped at `grid` blocks
 	uint32_t fcap = grid > 0 ? (uint32_t)grid
 				 : (uint32_t)(s_cus * occupancy((const void *)fast[ci][mi], s_focc[ci][mi], 8));
-#ifdef NSD_FAST_BPC
-	if (grid <= 0)
-		fcap = (uint32_t)(s_cus * NSD_FAST_BPC);   // experiments: fewer resident blocks than fit
-#endif
+	// with two tiles in flight per wave, 3 blocks per CU outrun the 4 that
+	// fit (HBM serves fewer concurrent streams better)
+	if (grid <= 0 && NSD_FAST_BPC > 0 && fcap > (uint32_t)(s_cus * NSD_FAST_BPC))
+		fcap = (uint32_t)(s_cus * NSD_FAST_BPC);
 	if (fcap > NSD_MAX_GRID)
 		fcap = NSD_MAX_GRID;
 	const uint32_t fblocks = want < fcap ? want : fcap;
