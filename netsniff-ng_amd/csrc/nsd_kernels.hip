@@ -1231,7 +1231,7 @@ constexpr int FROW = WIN1 / 4;   // fast rows: 16 dwords, 16-byte slots XOR-swiz
 #define NSD_FAST_BPC (NSD_FAST_DEPTH > 1 ? 3 : 0)   // resident fast blocks per CU (0: as many as fit)
 #endif
 #ifndef NSD_FAST_CSUM_U
-#define NSD_FAST_CSUM_U 4        // interior chunk loads in flight per lane (fast_icmp_pass)
+#define NSD_FAST_CSUM_U 8        // interior chunk loads in flight per lane (fast_icmp_pass; 4: C3 split +4 %)
 #endif
 
 struct FastShared {
