@@ -56,7 +56,10 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #define NSD_MINW 4                 // waves per SIMD the fused kernel is register-allocated for
 #endif
 #ifndef NSD_L2PF
-#define NSD_L2PF 16                // a tile with this many deferred packets touches tile t+2's lines
+#define NSD_L2PF 16                // a tile with this many deferred packets is walker-heavy (NSD_LATE)
+#endif
+#ifndef NSD_LATE
+#define NSD_LATE 1                 // a walker-heavy tile's successor loads its chunks after the walkers (0: before, with L2 touches)
 #endif
 #ifndef NSD_CSUM_SPLIT
 #define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
@@ -270,7 +273,8 @@ struct Chunks {
 // caplen too (stage_write zeroes them; a 64-byte window always lies inside
 // the frame buffer's NSD_FRAME_PAD): a load under a branch leaves hipcc
 // unsure whether it is pending, and it then waits vmcnt(0) for the chunks.
-template <int WIN, bool ALL = false>
+// NT: streaming loads; false where the general walk re-reads the lines soon.
+template <int WIN, bool ALL = false, bool NT = true>
 __device__ __forceinline__ void stage_load(Chunks<WIN> &ch, const uint8_t *frames, uint64_t my_desc, int lane)
 {
 	constexpr int CPP = Chunks<WIN>::CPP;
@@ -289,7 +293,11 @@ __device__ __forceinline__ void stage_load(Chunks<WIN> &ch, const uint8_t *frame
 			// streaming loads (nt): C2 -9 %, C3 -2 %; C4 +5 % (its general
 			// walk re-reads the first line from HBM rather than L2)
 			const uint64_t src = ((uint64_t)(ahr & 0xFFFFFFu) << 32 | alo) + pos;
-			const v4u t4 = __builtin_nontemporal_load((const gv4u *)src);
+			v4u t4;
+			if constexpr (NT)
+				t4 = __builtin_nontemporal_load((const gv4u *)src);
+			else
+				t4 = *(const gv4u *)src;
 			ch.v[r] = make_uint4(t4.x, t4.y, t4.z, t4.w);
 		} else {
 			ch.v[r] = make_uint4(0, 0, 0, 0);
@@ -912,6 +920,9 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	wk.have = false;
 	wk.stage = false;
 
+	// late: the next tile's chunks load after this tile's walkers (this tile's
+	// predecessor was walker-heavy: NSD_LATE, below)
+	bool late = false;
 	// (one more pass after the last tile drains the walkers: the engine is
 	// inlined once)
 	for (;; base += stride) {
@@ -930,7 +941,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			const uint32_t b2 = base + 2 * stride;
 			d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
 			const uint32_t b1 = base + stride;
-			if (b1 < n)
+			if (b1 < n && !late)
 				stage_load<WIN1>(ch, frames, d1, lane);
 			wave_sync_lds();
 
@@ -1015,18 +1026,26 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, pnd, w, i, d0, last);
 		if (last)
 			break;
-		// While the walkers are busy (C4), the lines of tile t+2 go into L2
-		// now, so the next iteration's loads of them wait for L2 rather than
-		// HBM: the walkers' first window wait (s_waitcnt vmcnt(0)) also
-		// waits for those loads (C4 1.45 -> 1.32 ms).  Not for tiles the
-		// fast walk finishes (C2, C3): there the next loads would wait for
-		// the touches (vector memory counts in order; C2 +12 %).  The
-		// LDS-DMA target is window words past the fast rows.
+		// After a walker-heavy tile (C4) the next tile's chunks load here, with
+		// L2-allocating loads, rather than a tile ahead: its walkers' first
+		// windows then find the packets' first lines in L2 (loaded a tile
+		// ahead, those lines had left L2 by the time the walkers staged them:
+		// C4 400 -> 349 B/packet, 1.152 -> 1.107 ms on one box).  The chunk
+		// registers are dead during the walkers either way.
+		if (late && base + stride < n)
+			stage_load<WIN1, false, false>(ch, frames, d1, lane);
+		// (NSD_LATE 0: the chunks load a tile ahead, and while the walkers are
+		// busy the lines of tile t+2 go into L2 now, so the next iteration's
+		// loads of them wait for L2 rather than HBM: C4 1.45 -> 1.32 ms then.
+		// Not for tiles the fast walk finishes (C2, C3): there the next loads
+		// would wait for the touches (vector memory counts in order; C2
+		// +12 %).  The LDS-DMA target is window words past the fast rows.)
 		{
 			const uint32_t b2 = base + 2 * stride;
-			if (many && b2 < n)
+			if (!NSD_LATE && many && b2 < n)
 				l2_touch(frames, d2, &s_win[wv][64 * ROW], b2 + lane < n);
 		}
+		late = NSD_LATE && many;
 		d0 = d1;
 		d1 = d2;
 	}
