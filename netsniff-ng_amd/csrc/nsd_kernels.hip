@@ -1297,6 +1297,56 @@ __device__ __forceinline__ uint32_t fold_weighted(uint32_t sum, bool odd)
 	return odd ? ((sum & 0xFF) << 8 | sum >> 8) : sum;
 }
 
+// The plain IPv4 chain (PRINT_NORM, split schedule): Ethernet (type 0x0800,
+// no tag), IPv4 without options (first byte 0x45), then TCP or UDP, in a
+// frame of at least 42 bytes.  For such a packet fast_walk (nsd_walk.h) reads
+// bytes 12..33 and nothing past them, all inside the window, and ends with
+// the chain Ethernet, IPv4, TCP / UDP at offsets 0 / 14 / 34 (proto_ethernet.c,
+// proto_ipv4.c:34-204 incl. the total-length trim, proto_tcp.c / proto_udp.c).
+// plain_is tells from bytes 12..23 whether the packet is one; plain_walk
+// then reads bytes 12..35 (7 row dwords, byte funnel shifts) and gives
+// fast_walk's result from them alone (re-read rather than kept: registers).
+// A tile takes this path only when every valid lane's packet is plain
+// (wave-uniform), so a mixed tile runs fast_walk alone.
+__device__ __forceinline__ bool plain_is(const LSrc<true, WIN1> &s, uint32_t caplen)
+{
+	const uint32_t r = s.m + 12, j = r >> 2, sh = r & 3;
+	const uint32_t d12 = __builtin_amdgcn_alignbyte(s.dw(j + 1), s.dw(j), sh);
+	const uint32_t d20 = __builtin_amdgcn_alignbyte(s.dw(j + 3), s.dw(j + 2), sh);
+	const uint32_t proto = d20 >> 24;
+	return caplen >= 42 && (d12 & 0xFFFFFFu) == 0x450008u && (proto == 6 || proto == 17);
+}
+
+__device__ __forceinline__ void plain_walk(const LSrc<true, WIN1> &s, uint32_t caplen, WalkOut &w)
+{
+	const uint32_t r = s.m + 12, j = r >> 2, sh = r & 3;   // j + 6 <= 12: inside the 16-dword row
+	const uint32_t w0 = s.dw(j), w1 = s.dw(j + 1), w2 = s.dw(j + 2), w3 = s.dw(j + 3), w4 = s.dw(j + 4),
+		       w5 = s.dw(j + 5), w6 = s.dw(j + 6);
+	const uint32_t d12 = __builtin_amdgcn_alignbyte(w1, w0, sh), d16 = __builtin_amdgcn_alignbyte(w2, w1, sh),
+		       d20 = __builtin_amdgcn_alignbyte(w3, w2, sh), d24 = __builtin_amdgcn_alignbyte(w4, w3, sh),
+		       d28 = __builtin_amdgcn_alignbyte(w5, w4, sh), d32 = __builtin_amdgcn_alignbyte(w6, w5, sh);
+	// calc_csum over the 10 header words at 14..32 (csum.h:12-27)
+	uint32_t sum = (d12 >> 16) + (d32 & 0xFFFF);
+	sum = __builtin_amdgcn_sad_u16(d16, 0u, sum);
+	sum = __builtin_amdgcn_sad_u16(d20, 0u, sum);
+	sum = __builtin_amdgcn_sad_u16(d24, 0u, sum);
+	sum = __builtin_amdgcn_sad_u16(d28, 0u, sum);
+	sum = (sum >> 16) + (sum & 0xffff);
+	sum += sum >> 16;
+	w.ip_csum = (uint16_t)~sum;
+	// the total-length trim (ihl 5: no options)
+	const int32_t x = (int32_t)__builtin_bswap16((uint16_t)d16) - 20;
+	if (x >= 0 && (uint32_t)x < caplen - 34)
+		w.tail = 34 + (uint32_t)x;
+	const bool tcp = (d20 >> 24) == 6;
+	const int l4 = tcp ? NSD_OPS_TCP : NSD_OPS_UDP;
+	w.chain = NSD_OPS_ETHERNET | NSD_OPS_IPV4 << 5 | (uint32_t)l4 << 10;
+	w.offA = (uint64_t)14 << 16 | (uint64_t)34 << 32;
+	w.n = 3;
+	const uint32_t len = w.tail - 34, hl = tcp ? 20u : 8u;
+	w.data = len >= hl ? 34 + hl : 34;
+}
+
 template <int MODE, bool CR>
 __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__restrict__ frames,
 					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
@@ -1364,9 +1414,15 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 		}
 		wave_sync_lds();
 		uint32_t fw = FW_DONE;
-		if (valid) {
-			const LSrc<true, WIN1> src{ rows + lane * FROW, sh.lay3, nullptr, frames + off, caplen,
-						    (uint32_t)off & 15, 0, false, swz_of((uint32_t)lane, 4) << 2 };
+		const LSrc<true, WIN1> src{ rows + lane * FROW, sh.lay3, nullptr, frames + off, caplen,
+					    (uint32_t)off & 15, 0, false, swz_of((uint32_t)lane, 4) << 2 };
+		// (every lane's row is staged, a lane past the batch from the clamped descriptor)
+		const bool plain = MODE == PRINT_NORM && start_id == NSD_OPS_ETHERNET &&
+				   __ballot(valid && !plain_is(src, caplen)) == 0;
+		if (plain) {
+			if (valid)
+				plain_walk(src, caplen, w);
+		} else if (valid) {
 			fw = fast_walk<MODE, true>(src, caplen, w);
 		}
 		const bool deferred = fw != FW_DONE;

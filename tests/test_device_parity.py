@@ -391,3 +391,45 @@ def test_walker_pool_mixed_tiles(grid, mode):
     assert np.array_equal(counters.cpu().numpy().view(np.uint64), ocnt)
     if grid == 0:
         _check_compact(frames, desc, mode)
+
+
+def _plain_tiles(seed=9, n=64 * 48):
+    """Ethernet / IPv4 (no options) / TCP or UDP frames only, so whole tiles
+    take the split fast kernel's plain path (plain_walk): frame lengths 42..
+    120, total lengths below the header, inside the frame (trimmed) and past
+    it, good and bad header checksums, TCP / UDP bodies shorter than their
+    headers."""
+    import random
+    rnd = random.Random(seed)
+    pkts = []
+    for k in range(n):
+        cap = rnd.choice([42, 43, 53, 54, 55, 60, 64, 64, 64, 90, 120])
+        proto = rnd.choice([6, 17])
+        r = rnd.random()
+        totlen = (rnd.randrange(0, 20) if r < 0.15 else rnd.randrange(cap - 14, cap + 30) if r < 0.4
+                  else rnd.randrange(20, cap - 14 + 1))
+        hdr = bytearray([0x45, rnd.randrange(256)]) + totlen.to_bytes(2, "big") + \
+            bytes(rnd.randrange(256) for _ in range(4)) + bytes([rnd.randrange(256), proto, 0, 0]) + \
+            bytes(rnd.randrange(256) for _ in range(8))
+        if rnd.random() < 0.5:
+            s = sum(int.from_bytes(hdr[i:i + 2], "big") for i in range(0, 20, 2))
+            while s >> 16:
+                s = (s & 0xFFFF) + (s >> 16)
+            hdr[10:12] = (~s & 0xFFFF).to_bytes(2, "big")
+        else:
+            hdr[10:12] = rnd.randrange(65536).to_bytes(2, "big")
+        eth = bytes(rnd.randrange(256) for _ in range(12)) + b"\x08\x00"
+        body = bytes(rnd.randrange(256) for _ in range(cap - 34))
+        pkts.append(eth + bytes(hdr) + body)
+    return pkts
+
+
+@pytest.mark.parametrize("align", [1, 2, 16])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_plain_tiles(mode, align):
+    """Tiles of plain IPv4 TCP / UDP frames (the split fast kernel's plain
+    path; the fused kernel's fast walk) at odd and even alignments: records
+    of both forms and counters equal the oracle's."""
+    frames, desc = T.batch_from_packets(_plain_tiles(), align=align)
+    _check(frames, desc, mode)
+    _check_compact(frames, desc, mode)
