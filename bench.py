@@ -399,8 +399,14 @@ def cpu_rate(cfg, n_sample, threads, seconds, text):
     """CPU restatement (oracle, "port") over one resident sample of
     `n_sample` packets, repeated until `seconds` have passed: fields only
     (records + counters) or fields + PRINT_NORM text (per-packet sink,
-    discarded like a write to /dev/null).  Returns (Mpkt/s, packets, s)."""
+    discarded like a write to /dev/null).  The text is what `netsniff-ng
+    --in` prints for the synthetic pcap the replay leg reads (records (i, 0)
+    timestamps): each packet's frame header line (show_frame_hdr), then the
+    dissector's.  Returns (Mpkt/s, packets, s)."""
     frames, desc = T.make_batch(cfg, n_sample, lo=0, threads=threads)
+    fh = np.zeros(n_sample, dtype=T.FH_DTYPE)
+    fh["sec"] = np.arange(n_sample, dtype=np.uint32)
+    fh["len"] = T.desc_caplen(desc).astype(np.uint32)
     lib = T.oracle()
     counters = np.zeros(64, dtype=np.uint64)
     rec = np.zeros(n_sample, dtype=T.REC_DTYPE)
@@ -408,8 +414,8 @@ def cpu_rate(cfg, n_sample, threads, seconds, text):
     done, t0 = 0, time.perf_counter()
     while True:
         if text:
-            lib.nsor_dissect_batch_text_mt(frames.ctypes.data, desc.ctypes.data, n_sample, 1, T.PRINT_NORM,
-                                           threads, tb.ctypes.data)
+            lib.nsor_dissect_batch_text_fh_mt(frames.ctypes.data, desc.ctypes.data, fh.ctypes.data, None, 1,
+                                              n_sample, 1, T.PRINT_NORM, threads, tb.ctypes.data)
         else:
             lib.nsor_dissect_batch_mt(frames.ctypes.data, desc.ctypes.data, n_sample, 1, T.PRINT_NORM,
                                       rec.ctypes.data, counters.ctypes.data, threads)
@@ -441,7 +447,8 @@ def cpu_baseline(key, seconds):
     else:
         tA, pA, dA, fA = tS, pS, dS, fS
     return {"value": round(tA, 3), "unit": "Mpkt/s", "cores": avail, "kind": "port",
-            "sample": f"{key}: fields + PRINT_NORM text (the reference prints as it parses) by the CPU "
+            "sample": f"{key}: fields + PRINT_NORM text with frame header lines (the reference prints as "
+                      f"it parses; `netsniff-ng --in`'s text) by the CPU "
                       f"restatement (oracle/nsd_oracle.c), {avail} threads (every available core) over "
                       f"contiguous shards, {pA} packets (passes over a resident "
                       f"{max(1 << 20, 4096 * avail) if more else 1 << 20}-packet sample) in {dA:.1f} s",
@@ -694,9 +701,9 @@ def main():
 
     rank, world, local = nsd_dist.rank_env()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # no launcher: start the N ranks here, as fresh processes, before this
-        # one touches a GPU (counting devices initialises none)
-        have = torch.cuda.device_count()
+        # no launcher: start the N ranks here, as fresh processes; this one
+        # never touches a GPU (the devices are counted in a child process)
+        have = nsd_dist.count_devices()
         if have < args.gpus:
             print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr)
             sys.exit(2)

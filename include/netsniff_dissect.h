@@ -477,6 +477,48 @@ long nsd_format_range_compact(const uint8_t *frames, const nsd_desc_t *desc, con
 			      uint32_t lo, uint32_t hi, int linktype, int mode, const nsd_crec *crec,
 			      const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends, int8_t *rc);
 
+/* ---- the frame header line (show_frame_hdr / __show_frame_hdr,
+ * dissector.h:31-116) ----------------------------------------------------------
+ * Every capture loop prints it right before it calls dissector_entry_point
+ * for a packet: read_pcap (netsniff-ng.c:732), walk_t3_block (:1021), the
+ * TPACKET_V2 ring loop (:1153), the forwarding loops (:368, :538).
+ * nsd_frame_hdr_t holds what __show_frame_hdr reads from the tpacket header:
+ *   - v3 == 0: a struct tpacket2_hdr, as read_pcap fills its frame_map
+ *     (zeroed once, netsniff-ng.c:672) with pcap_pkthdr_to_tpacket_hdr
+ *     (pcap_io.h:594-709): tp_len, tp_sec, tp_nsec per record format,
+ *     tp_status 0.  Built with HAVE_TPACKET3, tpacket_has_vlan_info reads
+ *     the status through the tpacket3_hdr view (ring.h:71-84), i.e. this
+ *     header's tp_nsec: a nsec value with bit 4 or 6 set prints the
+ *     " [ tpacketv3 VLAN ... ]" line with tci 0 / proto 0;
+ *   - v3 == 1: the frame's struct tpacket3_hdr in a TPACKET_V3 block
+ *     (tp_len, tp_sec, tp_nsec, tp_status, hv1.tp_vlan_tci / tp_vlan_tpid).
+ * The sockaddr_ll gives the packet type ("<", "B", "M", "P", ">", "K->U",
+ * "U->K", else "?") and the interface (if_indextoname, "?" when it fails);
+ * a LINKTYPE_NETLINK packet of >= 16 bytes marked PACKET_OUTGOING is shown
+ * as kernel / user by its nlmsg_pid (dissector.h:71-75).
+ * nsd_format_frame_hdr: the line for one packet (`count` = the loop's
+ * packet counter, 1 for the first); NUL-terminated when room, returns its
+ * length (PRINT_NONE: 0).
+ * nsd_format_range_compact_fh: nsd_format_range_compact with each packet's
+ * frame header in front of its text (fh[i], sll[i] (NULL: zeros), count
+ * first_count + i); fh NULL = nsd_format_range_compact. */
+typedef struct nsd_frame_hdr {
+	uint32_t len;        /* tp_len */
+	uint32_t sec;        /* tp_sec */
+	uint32_t nsec;       /* tp_nsec */
+	uint32_t status;     /* tp_status */
+	uint32_t vlan_tci;   /* v3: hv1.tp_vlan_tci */
+	uint16_t vlan_tpid;  /* v3: hv1.tp_vlan_tpid */
+	uint8_t  v3;         /* 1: tpacket3_hdr (walk_t3_block), 0: tpacket2_hdr */
+	uint8_t  reserved;
+} nsd_frame_hdr_t;
+long nsd_format_frame_hdr(const nsd_frame_hdr_t *fh, const nsd_sll_t *sll, const uint8_t *pkt,
+			  uint32_t caplen, int linktype, int mode, uint64_t count, char *out, size_t cap);
+long nsd_format_range_compact_fh(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+				 const nsd_frame_hdr_t *fh, uint64_t first_count, uint32_t lo, uint32_t hi,
+				 int linktype, int mode, const nsd_crec *crec, const uint32_t *ext_pool,
+				 char *out, size_t cap, uint64_t *ends, int8_t *rc);
+
 /* ---- pcap replay front end (`netsniff-ng --in f.pcap`, read_pcap
  * netsniff-ng.c:640-770; pcap_io.h / pcap_sg.c record formats) ---------------
  * nsd_pcap_open: validates the file header (tcpdump usec / nsec, Kuznetzov,
@@ -507,6 +549,15 @@ long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *d
  * header, zeros for other record forms. */
 long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
 			     nsd_sll_t *sll, uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns);
+/* as nsd_pcap_read_batch_sll, also filling fh[k] (may be NULL) with the
+ * tpacket2_hdr fields read_pcap prints (pcap_pkthdr_to_tpacket_hdr,
+ * pcap_io.h:594-709: tp_nsec = usec * 1000 for the usec and Kuznetzov
+ * forms, the ns field for nsec / Borkmann, byte-swapped files swapped, *_LL
+ * lengths minus the 16-byte cooked header), and sll[k] with every field that
+ * conversion sets: the cooked header (*_LL), ifindex / protocol / pkttype
+ * (Kuznetzov), ifindex / protocol / hatype / pkttype (Borkmann). */
+long nsd_pcap_read_batch_fh(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
+			    nsd_sll_t *sll, nsd_frame_hdr_t *fh, uint32_t max_n);
 void nsd_pcap_close(nsd_pcap *p);
 long nsd_replay_pcap(const char *path, int mode, const struct nsd_bpf_prog *filter, int out_fd,
 		     int cols, uint64_t *counters, int threads);
@@ -534,6 +585,11 @@ long nsd_t3_block_desc(const uint8_t *block, size_t block_len, int packet_type, 
  * (hdr + 48) into sll[k] (may be NULL), for the SLL heads */
 long nsd_t3_block_desc_sll(const uint8_t *block, size_t block_len, int packet_type,
 			   int lo_ifindex, nsd_desc_t *desc, nsd_sll_t *sll, uint32_t max_n);
+/* as nsd_t3_block_desc_sll, also filling fh[k] (may be NULL) from each kept
+ * frame's tpacket3_hdr (v3 = 1), what walk_t3_block's __show_frame_hdr
+ * prints (netsniff-ng.c:1021) */
+long nsd_t3_block_desc_fh(const uint8_t *block, size_t block_len, int packet_type, int lo_ifindex,
+			  nsd_desc_t *desc, nsd_sll_t *sll, nsd_frame_hdr_t *fh, uint32_t max_n);
 
 /* ---- classic BPF on the device --------------------------------
  * The capture loop filters every record before dissecting it (read_pcap

@@ -16,12 +16,17 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/netsniff_dissect.h"
 #include "nsd_lookup.h"
 #include "nsd_ntop.h"
+
+// as dissector.h:29 declares it (net/if.h and linux/if.h do not mix)
+extern "C" char *if_indextoname(unsigned ifindex, char *ifname);
 
 namespace nsd {
 
@@ -1157,7 +1162,106 @@ void format_post_dump(std::string &s, const uint8_t *pkt, uint32_t caplen, int m
 	}
 }
 
+// ---- show_frame_hdr (dissector.h:31-116) ----------------------------------
+
+// if_indextoname (dissector.h:82, 89), cached per interface index: the
+// reference asks the kernel for every packet (a socket and an ioctl); the
+// name of an index does not change while a capture runs.  Index 0 names no
+// interface.  Returns nullptr where if_indextoname fails.
+static const char *if_name(uint32_t idx)
+{
+	static std::mutex mu;
+	static std::unordered_map<uint32_t, std::string> names;   // "" = no such interface
+	thread_local uint32_t last = 0;
+	thread_local const std::string *last_name = nullptr;
+	if (idx == 0)
+		return nullptr;
+	if (idx != last || !last_name) {
+		std::lock_guard<std::mutex> g(mu);
+		auto it = names.find(idx);
+		if (it == names.end()) {
+			char b[32];
+			const char *r = if_indextoname(idx, b);
+			it = names.emplace(idx, r ? r : "").first;
+		}
+		last = idx;
+		last_name = &it->second;   // (map nodes do not move)
+	}
+	return last_name->empty() ? nullptr : last_name->c_str();
+}
+
+void format_frame_hdr(std::string &s, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, const uint8_t *pkt,
+		      uint32_t caplen, int linktype, int mode, uint64_t count)
+{
+	// packet_types[] (dissector.h:31-39)
+	static const char *const types[8] = { "<", "B", "M", "P", ">", nullptr, "K->U", "U->K" };
+	if (mode == PRINT_NONE)
+		return;
+	uint8_t pkttype = sll ? sll->pkttype : 0;
+	// nlmon captures: sll_pkttype is PACKET_OUTGOING for every packet; the
+	// nlmsg_pid tells kernel from user (dissector.h:71-75; the link type
+	// compared as passed, unswapped)
+	if ((uint32_t)linktype == NSD_LINKTYPE_NETLINK && caplen >= 16 && pkttype == 4) {
+		uint32_t pid;
+		memcpy(&pid, pkt + 12, 4);
+		pkttype = pid == 0 ? 7 : 6;
+	}
+	const char *pt = pkttype < 8 && types[pkttype] ? types[pkttype] : "?";
+	const char *ifn = if_name(sll ? (uint32_t)sll->ifindex : 0);
+	Out o(s);
+	o << pt;
+	o.c(' ') << (ifn ? ifn : "?");
+	o.c(' ').u(fh.len);
+	if (mode == PRINT_LESS) {
+		o << " #";
+		o.u(count);
+		return;
+	}
+	o.c(' ').u(fh.sec) << "s.";
+	o.u(fh.nsec) << "ns #";
+	o.u(count).c(' ');
+	if (!fh.v3) {
+		// __show_ts_source (dissector.h:41-51)
+		if (fh.status & 0x80000000u)
+			o << "(raw hw ts)";
+		else if (fh.status & 0x40000000u)
+			o << "(sys hw ts)";
+		else if (fh.status & 0x20000000u)
+			o << "(sw ts)";
+	}
+	o.c('\n');
+	// tpacket_has_vlan_info (ring.h:71-84): TP_STATUS_VLAN_VALID (1 << 4) |
+	// TP_STATUS_VLAN_TPID_VALID (1 << 6) of the tpacket3_hdr view's tp_status,
+	// which for a tpacket2_hdr is its tp_nsec; the tci / tpid helpers give 0
+	// for v2 (ring.h:51-69)
+	const uint32_t st = fh.v3 ? fh.status : fh.nsec;
+	if (st & 0x50u) {
+		const uint16_t tci = fh.v3 ? (uint16_t)fh.vlan_tci : 0;
+		const uint16_t tpid = fh.v3 ? fh.vlan_tpid : 0;
+		o << " [ tpacketv3 VLAN Prio (";
+		o.u((tci & 0xe000u) >> 13) << "), CFI (";
+		o.u((tci & 0x1000u) >> 12) << "), ID (";
+		o.u(tci & 0x0fffu) << "), Proto (0x";
+		o.xn(tpid, 4) << ") ]\n";
+	}
+}
+
 } // namespace nsd
+
+extern "C" long nsd_format_frame_hdr(const nsd_frame_hdr_t *fh, const nsd_sll_t *sll, const uint8_t *pkt,
+				     uint32_t caplen, int linktype, int mode, uint64_t count, char *out, size_t cap)
+{
+	if (!fh || (!pkt && caplen))
+		return NSD_ERR_ARG;
+	std::string s;
+	nsd::format_frame_hdr(s, *fh, sll, pkt, caplen, linktype, mode, count);
+	if (out && cap) {
+		const size_t k = s.size() < cap - 1 ? s.size() : cap - 1;
+		memcpy(out, s.data(), k);
+		out[k] = 0;
+	}
+	return (long)s.size();
+}
 
 extern "C" long nsd_format_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
 				  const nsd_rec *rec, const uint32_t *ext_pool, char *out, size_t cap)
@@ -1236,25 +1340,41 @@ extern "C" long nsd_format_range_compact(const uint8_t *frames, const nsd_desc_t
 					 uint32_t lo, uint32_t hi, int linktype, int mode, const nsd_crec *crec,
 					 const uint32_t *ext_pool, char *out, size_t cap, uint64_t *ends, int8_t *rc)
 {
+	return nsd_format_range_compact_fh(frames, desc, sll, nullptr, 0, lo, hi, linktype, mode, crec, ext_pool, out,
+					   cap, ends, rc);
+}
+
+extern "C" long nsd_format_range_compact_fh(const uint8_t *frames, const nsd_desc_t *desc, const nsd_sll_t *sll,
+					    const nsd_frame_hdr_t *fh, uint64_t first_count, uint32_t lo, uint32_t hi,
+					    int linktype, int mode, const nsd_crec *crec, const uint32_t *ext_pool,
+					    char *out, size_t cap, uint64_t *ends, int8_t *rc)
+{
 	if (hi < lo || (hi > lo && (!frames || !desc || !crec)))
 		return NSD_ERR_ARG;
 	// a per-thread buffer that keeps its capacity across calls (reserving
 	// `cap` per call faulted in fresh pages every time: threads formatting
-	// ranges in parallel then queued on the process's page-table lock)
+	// ranges in parallel then queued on the process's page-table lock);
+	// given back when it grew far past what this call needed
 	static thread_local std::string t_buf;
 	std::string &s = t_buf;
 	s.clear();
 	for (uint32_t i = lo; i < hi; i++) {
 		const uint64_t d = desc[i];
-		int r = nsd::format_packet_compact(s, frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), linktype, mode,
-						   crec[i], i, ext_pool, sll ? sll + i : nullptr);
+		const uint8_t *pkt = frames + NSD_DESC_OFF(d);
+		if (fh)
+			nsd::format_frame_hdr(s, fh[i], sll ? sll + i : nullptr, pkt, NSD_DESC_CAPLEN(d), linktype, mode,
+					      first_count + i);
+		int r = nsd::format_packet_compact(s, pkt, NSD_DESC_CAPLEN(d), linktype, mode, crec[i], i, ext_pool,
+						   sll ? sll + i : nullptr);
 		if (rc)
 			rc[i - lo] = (int8_t)r;
 		if (ends)
 			ends[i - lo] = s.size();
 	}
-	if (s.size() > cap)
-		return -(long)s.size();
-	memcpy(out, s.data(), s.size());
-	return (long)s.size();
+	const long total = (long)s.size();
+	if (s.size() <= cap)
+		memcpy(out, s.data(), s.size());
+	if (s.capacity() > ((size_t)64 << 20) && s.capacity() > 4 * s.size())
+		std::string().swap(s);
+	return total <= (long)cap ? total : -total;
 }

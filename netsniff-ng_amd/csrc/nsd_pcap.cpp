@@ -43,6 +43,8 @@
 #include "../../include/netsniff_dissect.h"
 
 namespace nsd {
+void format_frame_hdr(std::string &s, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, const uint8_t *pkt,
+		      uint32_t caplen, int linktype, int mode, uint64_t count);
 int render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
 		      const nsd_sll_t *sll);
 int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
@@ -71,6 +73,7 @@ struct nsd_pcap {
 	uint32_t ll_extra = 0;   // cooked-header bytes counted in caplen (*_LL)
 	uint32_t linktype = 0;   // as stored in the file header
 	uint32_t magic_raw = 0;  // as stored in the file header
+	uint32_t magic = 0;      // in host order
 	bool nsec = false;
 	bool eof = false;
 	// buffered reader (the scatter-gather reader's iovecs, pcap_sg.c)
@@ -141,6 +144,7 @@ extern "C" nsd_pcap *nsd_pcap_open(const char *path)
 	}
 	const uint32_t lt_host = p->swapped ? bswap32(lt) : lt;
 	p->linktype = lt;
+	p->magic = m;
 	p->nsec = m == NSEC || m == BKM;
 	if (m == KUZ || m == BKM) {
 		p->hdrsize = 24;
@@ -174,6 +178,55 @@ extern "C" long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, ns
 	return nsd_pcap_read_batch_sll(p, frames, cap, desc, nullptr, max_n, wire_len, ts_ns);
 }
 
+// What read_pcap's pcap_pkthdr_to_tpacket_hdr (pcap_io.h:594-709) makes of
+// one record header h (as stored) in its frame_map, zeroed once
+// (netsniff-ng.c:672) and overwritten field by field per record:
+//   tp_sec = ts.tv_sec; tp_nsec = tv_usec * 1000 (usec, *_LL, Kuznetzov) or
+//   the ns field (nsec, Borkmann); tp_len = len, minus the cooked header for
+//   *_LL; all byte-swapped for swapped files (the usec product in 32 bits);
+//   sll: the cooked header (*_LL: ll_to_sockaddr, pcap_io.h:182-191:
+//   pkttype / hatype / halen from be16, protocol as stored, addr), or the
+//   Kuznetzov ifindex / protocol / pkttype, or the Borkmann ifindex (u16) /
+//   protocol / hatype / pkttype; every other field stays 0.
+static void record_meta(const nsd_pcap *p, const uint8_t *h, nsd_sll_t *sll, nsd_frame_hdr_t *fh)
+{
+	const bool sw = p->swapped;
+	auto r32 = [&](int o) { uint32_t v; memcpy(&v, h + o, 4); return sw ? bswap32(v) : v; };
+	auto r16 = [&](int o) { uint16_t v; memcpy(&v, h + o, 2); return sw ? bswap16(v) : v; };
+	if (fh) {
+		memset(fh, 0, sizeof(*fh));
+		fh->sec = r32(0);
+		const uint32_t frac = r32(4);
+		fh->nsec = p->nsec ? frac : frac * 1000u;
+		fh->len = r32(12) - p->ll_extra;
+	}
+	if (!sll)
+		return;
+	nsd_sll_t ll;
+	memset(&ll, 0, sizeof(ll));
+	if (p->ll_extra) {
+		const uint8_t *c = h + 16;   // struct pcap_ll, big-endian fields
+		ll.pkttype = (uint8_t)(((uint32_t)c[0] << 8) | c[1]);
+		ll.hatype = (uint16_t)(((uint32_t)c[2] << 8) | c[3]);
+		ll.halen = (uint8_t)(((uint32_t)c[4] << 8) | c[5]);
+		memcpy(ll.addr, c + 6, 8);
+		memcpy(&ll.protocol, c + 14, 2);
+	} else if (p->magic == KUZ) {
+		// struct pcap_pkthdr_kuz {ts, caplen, len, u32 ifindex, u16 protocol, u8 pkttype}
+		ll.ifindex = (int32_t)r32(16);
+		ll.protocol = r16(20);
+		ll.pkttype = h[22];
+	} else if (p->magic == BKM) {
+		// struct pcap_pkthdr_bkm {ts, caplen, len, u16 tsource, u16 ifindex,
+		// u16 protocol, u8 hatype, u8 pkttype}
+		ll.ifindex = r16(18);
+		ll.protocol = r16(20);
+		ll.hatype = h[22];
+		ll.pkttype = h[23];
+	}
+	*sll = ll;
+}
+
 // same, also filling sll[k] (may be NULL) the way read_pcap fills fm.s_ll
 // (netsniff-ng.c:672, 727): zeroed once, then for *_LL records
 // pcap_pkthdr_to_tpacket_hdr -> ll_to_sockaddr (pcap_io.h:182-191, 594-660)
@@ -182,18 +235,24 @@ extern "C" long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, ns
 // file byte order): pkttype / hatype / halen from be16, protocol kept as
 // stored (be16), addr copied; family and ifindex stay 0.
 static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc, nsd_sll_t *sll,
-		       uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns, uint8_t *rhdr);
+		       nsd_frame_hdr_t *fh, uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns, uint8_t *rhdr);
 
 extern "C" long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
 					nsd_sll_t *sll, uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns)
 {
-	return read_batch(p, frames, cap, desc, sll, max_n, wire_len, ts_ns, nullptr);
+	return read_batch(p, frames, cap, desc, sll, nullptr, max_n, wire_len, ts_ns, nullptr);
+}
+
+extern "C" long nsd_pcap_read_batch_fh(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
+				       nsd_sll_t *sll, nsd_frame_hdr_t *fh, uint32_t max_n)
+{
+	return read_batch(p, frames, cap, desc, sll, fh, max_n, nullptr, nullptr, nullptr);
 }
 
 // rhdr (may be NULL): each record's header bytes as stored (hdrsize <= 32,
 // 32-byte stride), for the pcap write-out
 static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc, nsd_sll_t *sll,
-		       uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns, uint8_t *rhdr)
+		       nsd_frame_hdr_t *fh, uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns, uint8_t *rhdr)
 {
 	if (!p || !frames || !desc || cap < NSD_FRAME_PAD)
 		return NSD_ERR_ARG;
@@ -242,19 +301,8 @@ static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *des
 		desc[n] = NSD_DESC(at, caplen);
 		if (rhdr)
 			memcpy(rhdr + 32 * (size_t)n, h, p->hdrsize);
-		if (sll) {
-			nsd_sll_t ll;
-			memset(&ll, 0, sizeof(ll));
-			if (p->ll_extra) {
-				const uint8_t *c = h + 16;   // struct pcap_ll
-				ll.pkttype = (uint8_t)(((uint32_t)c[0] << 8) | c[1]);
-				ll.hatype = (uint16_t)(((uint32_t)c[2] << 8) | c[3]);
-				ll.halen = (uint8_t)(((uint32_t)c[4] << 8) | c[5]);
-				memcpy(ll.addr, c + 6, 8);
-				memcpy(&ll.protocol, c + 14, 2);
-			}
-			sll[n] = ll;
-		}
+		if (sll || fh)
+			record_meta(p, h, sll ? sll + n : nullptr, fh ? fh + n : nullptr);
 		if (wire_len)
 			wire_len[n] = wl;
 		if (ts_ns)
@@ -268,9 +316,10 @@ static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *des
 
 // The next record whatever its length (<= the 1 MiB replay buffer), for the
 // records a batch cannot carry: its bytes into `frame`, its header as stored
-// into rhdr (may be NULL), its cooked header into *sll.  Returns caplen, 0 at
-// the end of the replay.
-static long read_one(nsd_pcap *p, std::vector<uint8_t> &frame, nsd_sll_t *sll, uint8_t *rhdr)
+// into rhdr (may be NULL), its sockaddr_ll / frame header fields into *sll /
+// *fh (record_meta).  Returns caplen, 0 at the end of the replay.
+static long read_one(nsd_pcap *p, std::vector<uint8_t> &frame, nsd_sll_t *sll, nsd_frame_hdr_t *fh,
+		     uint8_t *rhdr)
 {
 	if (p->eof || !p->fill(p->hdrsize)) {
 		p->eof = true;
@@ -291,17 +340,7 @@ static long read_one(nsd_pcap *p, std::vector<uint8_t> &frame, nsd_sll_t *sll, u
 	frame.resize((size_t)caplen + NSD_FRAME_PAD, 0);
 	if (rhdr)
 		memcpy(rhdr, h, p->hdrsize);
-	nsd_sll_t ll;
-	memset(&ll, 0, sizeof(ll));
-	if (p->ll_extra) {
-		const uint8_t *c = h + 16;
-		ll.pkttype = (uint8_t)(((uint32_t)c[0] << 8) | c[1]);
-		ll.hatype = (uint16_t)(((uint32_t)c[2] << 8) | c[3]);
-		ll.halen = (uint8_t)(((uint32_t)c[4] << 8) | c[5]);
-		memcpy(ll.addr, c + 6, 8);
-		memcpy(&ll.protocol, c + 14, 2);
-	}
-	*sll = ll;
+	record_meta(p, h, sll, fh);
 	p->pos += p->hdrsize + caplen;
 	return caplen;
 }
@@ -380,6 +419,8 @@ struct ReplayRes {
 		nsd_crec *rec;
 		uint32_t *ext;
 	} buf[NSLOT] = {};
+	// each record's frame header fields (show_frame_hdr)
+	std::vector<nsd_frame_hdr_t> fh[NSLOT];
 	// the formatter parts' text buffers per slot, kept with their capacity:
 	// regrown per replay they faulted in hundreds of MB of fresh pages,
 	// with the formatter threads queued on the page-table lock
@@ -401,6 +442,8 @@ struct ReplayRes {
 				return NSD_ERR_NOMEM;
 			}
 		}
+		for (auto &v : fh)
+			v.resize(BATCH);
 		return NSD_OK;
 	}
 	void release()
@@ -415,6 +458,8 @@ struct ReplayRes {
 		}
 		for (auto &v : part)
 			std::vector<std::string>().swap(v);
+		for (auto &v : fh)
+			std::vector<nsd_frame_hdr_t>().swap(v);
 		nsd_pipe_destroy(pipe);
 		pipe = nullptr;
 	}
@@ -454,7 +499,10 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	if (!p)
 		return NSD_ERR_ARG;
 	const int lt = (int)p->linktype;
-	const bool has_ll = p->ll_extra != 0;   // *_LL file: one sockaddr_ll per record
+	// the dissector's SLL head reads the sockaddr_ll: an *_LL file's cooked
+	// headers, or a Kuznetzov / Borkmann file of an SLL link type (the frame
+	// headers read it for every file)
+	const bool has_ll = p->ll_extra != 0 || p->linktype == LT_LINUX_SLL || p->linktype == bswap32(LT_LINUX_SLL);
 	if (pcap_fd >= 0 && !push_fhdr(p, pcap_fd)) {
 		nsd_pcap_close(p);
 		return NSD_ERR_ARG;
@@ -477,6 +525,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		nsd_desc_t *desc = nullptr;
 		nsd_sll_t *sll = nullptr;
 		uint8_t *rhdr = nullptr;   // record headers as read (pcap write-out)
+		nsd_frame_hdr_t *fh = nullptr;
+		uint64_t count0 = 0;       // the packet counter of the batch's first record
 		nsd_crec *rec = nullptr;
 		uint32_t *ext = nullptr;
 		uint32_t *verdict = nullptr;
@@ -497,7 +547,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		x.desc = res.buf[k].desc;
 		x.rec = res.buf[k].rec;
 		x.ext = res.buf[k].ext;
-		x.sll = has_ll ? res.buf[k].sll : nullptr;
+		x.sll = res.buf[k].sll;
+		x.fh = res.fh[k].data();
 		x.verdict = filter ? &verdicts[(size_t)k * BATCH] : nullptr;
 		x.rhdr = pcap_fd >= 0 ? &rhdrs[(size_t)k * BATCH * 32] : nullptr;
 		x.part = &res.part[k];
@@ -516,6 +567,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	long err = rc;                          // first error of any stage
 	bool stop = false;
 	long printed = 0;
+	uint64_t counted = 0;                   // read_pcap's ctx->tx_packets (netsniff-ng.c:730)
 	long wrap_state = 0;
 	std::string wrapped;
 
@@ -582,9 +634,12 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		s.clear();
 		for (uint32_t k = lo; k < hi; k++) {
 			const uint64_t d = x.desc[k];
+			// show_frame_hdr, then the entry point (netsniff-ng.c:732-737)
+			nsd::format_frame_hdr(s, x.fh[k], x.sll + k, x.frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), lt, mode,
+					      x.count0 + k);
 			const size_t mark = s.size();
 			const int r = nsd::format_packet_compact(s, x.frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), lt, mode,
-								 x.rec[k], k, x.ext, x.sll ? x.sll + k : nullptr);
+								 x.rec[k], k, x.ext, x.sll + k);
 			if (r == NSD_OK)
 				continue;
 			// a record that could not hold its chain (NSD_F_OVERFLOW: longer
@@ -595,7 +650,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 				return NSD_ERR_FORMAT;
 			s.resize(mark);
 			const int r2 = nsd::render_packet_cpu(s, x.frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), lt, mode,
-							      x.sll ? x.sll + k : nullptr);
+							      x.sll + k);
 			if (r2 != NSD_OK)
 				return r2;
 		}
@@ -692,8 +747,9 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		if (r != NSD_OK)
 			return r;
 		nsd_sll_t ll;
+		nsd_frame_hdr_t fh;
 		uint8_t hdr[32];
-		const long caplen = read_one(p, big, &ll, hdr);
+		const long caplen = read_one(p, big, &ll, &fh, hdr);
 		if (caplen <= 0)
 			return NSD_OK;
 		if (filter) {
@@ -708,7 +764,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		if (counters)
 			nsd::cpu_count_packet(big.data(), (uint32_t)caplen, lt, mode, has_ll ? &ll : nullptr, counters);
 		std::string text;
-		r = nsd::render_packet_cpu(text, big.data(), (size_t)caplen, lt, mode, has_ll ? &ll : nullptr);
+		nsd::format_frame_hdr(text, fh, &ll, big.data(), (uint32_t)caplen, lt, mode, ++counted);
+		r = nsd::render_packet_cpu(text, big.data(), (size_t)caplen, lt, mode, &ll);
 		if (r != NSD_OK)
 			return r;
 		// (the writer is idle: every batch before this record is written)
@@ -746,7 +803,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			std::lock_guard<std::mutex> g(mu);
 			free_slots.push_back(k);
 		};
-		long n = read_batch(p, x.frames, FRAME_BYTES, x.desc, x.sll, BATCH, nullptr, nullptr, x.rhdr);
+		long n = read_batch(p, x.frames, FRAME_BYTES, x.desc, x.sll, x.fh, BATCH, nullptr, nullptr, x.rhdr);
 		if (n == NSD_ERR_CAPLEN) {
 			give_back();
 			rc = one_big();
@@ -774,8 +831,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			long m = 0;
 			for (long j = 0; j < n; j++)
 				if (x.verdict[j]) {
-					if (x.sll)
-						x.sll[m] = x.sll[j];
+					x.sll[m] = x.sll[j];
+					x.fh[m] = x.fh[j];
 					if (x.rhdr && m != j)
 						memcpy(x.rhdr + 32 * (size_t)m, x.rhdr + 32 * (size_t)j, 32);
 					x.desc[m++] = x.desc[j];
@@ -789,10 +846,12 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		if ((int)on_device.size() == DEPTH)
 			complete_oldest();
 		x.n = (uint32_t)n;
+		x.count0 = counted + 1;
+		counted += x.n;
 		x.status = NSD_OK;
 		memset(x.cnt, 0, sizeof(x.cnt));
-		int r = nsd_pipe_submit_compact(pipe, x.frames, used, x.desc, x.sll, x.n, x.rec, x.ext, &x.ext_used, x.cnt,
-						&x.status);
+		int r = nsd_pipe_submit_compact(pipe, x.frames, used, x.desc, has_ll ? x.sll : nullptr, x.n, x.rec, x.ext,
+						&x.ext_used, x.cnt, &x.status);
 		if (r != NSD_OK) {
 			give_back();
 			rc = r;
@@ -854,6 +913,16 @@ extern "C" long nsd_t3_block_desc(const uint8_t *block, size_t block_len, int pa
 extern "C" long nsd_t3_block_desc_sll(const uint8_t *block, size_t block_len, int packet_type,
 				      int lo_ifindex, nsd_desc_t *desc, nsd_sll_t *sll, uint32_t max_n)
 {
+	return nsd_t3_block_desc_fh(block, block_len, packet_type, lo_ifindex, desc, sll, nullptr, max_n);
+}
+
+// same, also the frame header fields walk_t3_block's __show_frame_hdr reads
+// from each kept frame's tpacket3_hdr (netsniff-ng.c:1021; v3 true):
+// tp_sec +4, tp_nsec +8, tp_len +16, tp_status +20, hv1.tp_vlan_tci +32,
+// hv1.tp_vlan_tpid +36
+extern "C" long nsd_t3_block_desc_fh(const uint8_t *block, size_t block_len, int packet_type, int lo_ifindex,
+				     nsd_desc_t *desc, nsd_sll_t *sll, nsd_frame_hdr_t *fh, uint32_t max_n)
+{
 	if (!block || !desc || block_len < 48)
 		return NSD_ERR_ARG;
 	uint32_t num_pkts, first;
@@ -879,6 +948,17 @@ extern "C" long nsd_t3_block_desc_sll(const uint8_t *block, size_t block_len, in
 				return NSD_ERR_ARG;
 			if (sll)
 				memcpy(&sll[n], block + h + 48, sizeof(nsd_sll_t));
+			if (fh) {
+				nsd_frame_hdr_t &f = fh[n];
+				memset(&f, 0, sizeof(f));
+				memcpy(&f.sec, block + h + 4, 4);
+				memcpy(&f.nsec, block + h + 8, 4);
+				memcpy(&f.len, block + h + 16, 4);
+				memcpy(&f.status, block + h + 20, 4);
+				memcpy(&f.vlan_tci, block + h + 32, 4);
+				memcpy(&f.vlan_tpid, block + h + 36, 2);
+				f.v3 = 1;
+			}
 			desc[n++] = NSD_DESC(h + mac, snaplen);
 		}
 		if (i + 1 < num_pkts) {

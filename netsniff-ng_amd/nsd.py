@@ -78,12 +78,18 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_replay_pcap_out", "nsd_build_info", "nsd_walk_packet_cpu", "nsd_set_etcdir",
                "nsd_dissect_device_compact", "nsd_format_batch_compact", "nsd_pipe_create_compact",
                "nsd_pipe_submit_compact", "nsd_format_range_compact", "nsd_set_schedule",
-               "nsd_last_schedule"]
+               "nsd_last_schedule", "nsd_format_frame_hdr", "nsd_format_range_compact_fh",
+               "nsd_pcap_read_batch_fh", "nsd_t3_block_desc_fh"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
                       ("pkttype", "u1"), ("halen", "u1"), ("addr", "u1", (8,))])
 LINKTYPE_LINUX_SLL = 113
+LINKTYPE_NETLINK = 253
+
+# nsd_frame_hdr_t: the tpacket header fields show_frame_hdr prints
+FH_DTYPE = np.dtype([("len", "<u4"), ("sec", "<u4"), ("nsec", "<u4"), ("status", "<u4"), ("vlan_tci", "<u4"),
+                     ("vlan_tpid", "<u2"), ("v3", "u1"), ("reserved", "u1")])
 
 _lib = None
 _vp, _u32, _u64, _int, _sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
@@ -204,6 +210,11 @@ def lib():
                 ("nsd_format_range_compact", ctypes.c_long,
                  [_vp, _vp, _vp, _u32, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]),
                 ("nsd_set_schedule", _int, [_int]),
+                ("nsd_format_frame_hdr", ctypes.c_long, [_vp, _vp, _vp, _u32, _int, _int, _u64, ctypes.c_char_p, _sz]),
+                ("nsd_format_range_compact_fh", ctypes.c_long,
+                 [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]),
+                ("nsd_pcap_read_batch_fh", ctypes.c_long, [_vp, _vp, _sz, _vp, _vp, _vp, _u32]),
+                ("nsd_t3_block_desc_fh", ctypes.c_long, [_vp, _sz, _int, _int, _vp, _vp, _vp, _u32]),
                 ("nsd_last_schedule", _int, [])):
             if hasattr(L, name):
                 getattr(L, name).restype = res
@@ -641,10 +652,59 @@ def pcap_read(path, cap=64 << 20, max_n=1 << 16, sll=False):
         L.nsd_pcap_close(h)
 
 
+def pcap_frame_hdrs(path, cap=64 << 20, max_n=1 << 16):
+    """Every record's frame header fields and sockaddr_ll as read_pcap holds
+    them (nsd_pcap_read_batch_fh): (linktype, packets [bytes], fh FH_DTYPE,
+    sll SLL_DTYPE)."""
+    L = lib()
+    h = L.nsd_pcap_open(os.fsencode(path))
+    if not h:
+        raise NsdError(f"nsd_pcap_open({path}) failed")
+    try:
+        lt = L.nsd_pcap_linktype(h)
+        pkts, fhs, slls = [], [], []
+        while True:
+            frames = np.zeros(cap, dtype=np.uint8)
+            desc = np.zeros(max_n, dtype=np.uint64)
+            fh = np.zeros(max_n, dtype=FH_DTYPE)
+            ll = np.zeros(max_n, dtype=SLL_DTYPE)
+            n = L.nsd_pcap_read_batch_fh(h, frames.ctypes.data, cap, desc.ctypes.data, ll.ctypes.data,
+                                         fh.ctypes.data, max_n)
+            if n < 0:
+                raise NsdError(f"nsd_pcap_read_batch_fh failed with status {n}")
+            if n == 0:
+                break
+            for d in desc[:n]:
+                d = int(d)
+                pkts.append(bytes(frames[d & 0xFFFFFFFFFF:(d & 0xFFFFFFFFFF) + (d >> 40)]))
+            fhs.append(fh[:n].copy())
+            slls.append(ll[:n].copy())
+        fh = np.concatenate(fhs) if fhs else np.zeros(0, dtype=FH_DTYPE)
+        ll = np.concatenate(slls).astype(SLL_DTYPE) if slls else np.zeros(0, dtype=SLL_DTYPE)
+        return lt, pkts, fh, ll
+    finally:
+        L.nsd_pcap_close(h)
+
+
+def format_frame_hdr(fh, pkt=b"", sll=None, linktype=LINKTYPE_EN10MB, mode=PRINT_NORM, count=1):
+    """show_frame_hdr's line for one packet (nsd_format_frame_hdr)."""
+    L = lib()
+    f = np.asarray(fh, dtype=FH_DTYPE).reshape(1)
+    s = None if sll is None else np.asarray(sll, dtype=SLL_DTYPE).reshape(1)
+    p = np.frombuffer(bytes(pkt) + b"\0", dtype=np.uint8)
+    buf = ctypes.create_string_buffer(512)
+    n = L.nsd_format_frame_hdr(f.ctypes.data, None if s is None else s.ctypes.data, p.ctypes.data, len(pkt),
+                               linktype, mode, count, buf, 512)
+    _check(0 if n >= 0 else n, "nsd_format_frame_hdr")
+    return buf.raw[:n]
+
+
 def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None, threads=0, out_fd=None,
                 pcap_out=None):
     """`netsniff-ng --in path` through the device: returns (records printed,
-    text bytes), or (records printed, None) when writing to out_fd.
+    text bytes), or (records printed, None) when writing to out_fd.  Each
+    packet's text is its frame header line (show_frame_hdr) followed by the
+    dissector's.
     prog: a BpfProgram (or None).  pcap_out: path of the `--out f.pcap`
     write-out (nsd_replay_pcap_out), or None."""
     import tempfile
@@ -669,13 +729,17 @@ def replay_pcap(path, mode=PRINT_NORM, prog=None, cols=0, counters=None, threads
             os.close(pfd)
 
 
-def t3_block_desc(block, packet_type=-1, lo_ifindex=-1, max_n=1 << 16, sll=False):
-    """Descriptors of a TPACKET_V3 block's frames (nsd_t3_block_desc_sll);
-    with sll=True also each kept frame's sockaddr_ll: (desc, sll)."""
+def t3_block_desc(block, packet_type=-1, lo_ifindex=-1, max_n=1 << 16, sll=False, fh=False):
+    """Descriptors of a TPACKET_V3 block's frames (nsd_t3_block_desc_fh);
+    with sll=True also each kept frame's sockaddr_ll, with fh=True its frame
+    header fields: desc, or a tuple (desc[, sll][, fh])."""
     block = np.ascontiguousarray(block, dtype=np.uint8)
     desc = np.zeros(max_n, dtype=np.uint64)
     ll = np.zeros(max_n, dtype=SLL_DTYPE)
-    n = lib().nsd_t3_block_desc_sll(block.ctypes.data, block.nbytes, packet_type, lo_ifindex,
-                                    desc.ctypes.data, ll.ctypes.data if sll else None, max_n)
-    _check(0 if n >= 0 else n, "nsd_t3_block_desc_sll")
-    return (desc[:n], ll[:n]) if sll else desc[:n]
+    f = np.zeros(max_n, dtype=FH_DTYPE)
+    n = lib().nsd_t3_block_desc_fh(block.ctypes.data, block.nbytes, packet_type, lo_ifindex,
+                                   desc.ctypes.data, ll.ctypes.data if sll else None,
+                                   f.ctypes.data if fh else None, max_n)
+    _check(0 if n >= 0 else n, "nsd_t3_block_desc_fh")
+    out = (desc[:n],) + ((ll[:n],) if sll else ()) + ((f[:n],) if fh else ())
+    return out if len(out) > 1 else out[0]

@@ -90,6 +90,17 @@ def max_over_ranks(values, device, group=None):
     return [float(x) for x in t]
 
 
+def count_devices():
+    """GPUs visible, counted in a child process so the caller initialises
+    no GPU runtime before it spawns its ranks (0 if the count fails)."""
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=300)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -101,7 +112,8 @@ def free_port():
 def spawn_ranks(nproc, script, argv, env=None):
     """Run `script argv` as `nproc` fresh rank processes, one per GPU, under
     torch.distributed.run on 127.0.0.1 (the caller has not touched a GPU:
-    counting devices does not initialise one), and return their exit code.
+    count_devices counts them in a child process), and return their exit
+    code.
     The ranks' stdout is this process's: rank 0 prints the result."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), script] + list(argv)

@@ -2020,9 +2020,202 @@ uint64_t nsor_dissect_batch_text(const uint8_t *frames, const nsd_desc_t *desc,
 	return sw;
 }
 
+/* ---- show_frame_hdr (dissector.h:31-116) ---------------------------------
+ * The line every capture loop prints before the entry point.  The header
+ * view: a tpacket2_hdr (v3 0, read_pcap's zeroed frame_map) or the frame's
+ * tpacket3_hdr (v3 1, walk_t3_block).  ring.h is built with HAVE_TPACKET3,
+ * so tpacket_has_vlan_info reads tp_status through the tpacket3_hdr view
+ * (ring.h:71-84): for a tpacket2_hdr that is the word at offset 20, tp_nsec;
+ * tpacket_uhdr_vlan_tci / _proto return 0 when v3 is false (ring.h:51-69). */
+extern char *if_indextoname(unsigned ifindex, char *ifname);
+
+static const char *const fh_packet_types[256] = {
+	[0] = "<", [1] = "B", [2] = "M", [3] = "P", [4] = ">", [6] = "K->U", [7] = "U->K",
+};
+
+static const char *fh_ts_source(uint32_t status)      /* dissector.h:41-51 */
+{
+	if (status & (1u << 31))
+		return "(raw hw ts)";
+	else if (status & (1u << 30))
+		return "(sys hw ts)";
+	else if (status & (1u << 29))
+		return "(sw ts)";
+	return "";
+}
+
+static void T(nsor_text *t, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static void T(nsor_text *t, const char *fmt, ...)
+{
+	char tmp[256];
+	va_list vl;
+	int n;
+	va_start(vl, fmt);
+	n = vsnprintf(tmp, sizeof(tmp), fmt, vl);
+	va_end(vl);
+	if (n > 0)
+		text_append(t, tmp, (size_t)n);
+}
+
+void nsor_frame_hdr(const nsd_frame_hdr_t *fh, const nsd_sll_t *sll, const uint8_t *pkt, uint32_t caplen,
+		    int linktype, int mode, uint64_t count, nsor_text *t)
+{
+	char tmp[64];
+	nsd_sll_t z;
+	uint8_t pkttype;
+	const char *ifn;
+
+	if (mode == PRINT_NONE)
+		return;
+	if (!sll) {
+		memset(&z, 0, sizeof(z));
+		sll = &z;
+	}
+	pkttype = sll->pkttype;
+	if (linktype == NSD_LINKTYPE_NETLINK && caplen >= 16 && pkttype == 4) {
+		uint32_t pid;
+		memcpy(&pid, pkt + 12, 4);                   /* nlmsghdr.nlmsg_pid */
+		pkttype = pid == 0 ? 7 : 6;                  /* PACKET_KERNEL : PACKET_USER */
+	}
+	ifn = if_indextoname((unsigned)sll->ifindex, tmp);
+	switch (mode) {
+	case PRINT_LESS:
+		T(t, "%s %s %u #%lu", fh_packet_types[pkttype] ? fh_packet_types[pkttype] : "?", ifn ? ifn : "?",
+		  fh->len, (unsigned long)count);
+		break;
+	default:
+		T(t, "%s %s %u %us.%uns #%lu %s\n", fh_packet_types[pkttype] ? fh_packet_types[pkttype] : "?",
+		  ifn ? ifn : "?", fh->len, fh->sec, fh->nsec, (unsigned long)count,
+		  fh->v3 ? "" : fh_ts_source(fh->status));
+		if ((fh->v3 ? fh->status : fh->nsec) & ((1u << 4) | (1u << 6))) {
+			uint16_t tci = fh->v3 ? (uint16_t)fh->vlan_tci : 0;
+			T(t, " [ tpacketv3 VLAN ");
+			T(t, "Prio (%u), ", (tci & 0xe000) >> 13);
+			T(t, "CFI (%u), ", (tci & 0x1000) >> 12);
+			T(t, "ID (%u), ", tci & 0x0fff);
+			T(t, "Proto (0x%.4x)", fh->v3 ? fh->vlan_tpid : 0);
+			T(t, " ]\n");
+		}
+		break;
+	}
+}
+
+/* ---- pcap records -> the frame_map read_pcap prints from ------------------
+ * pcap_validate_header (pcap_io.h:874-911: magic, version, the *_LL remap
+ * for SLL / netlink link types), the record sizes (pcap_get_hdr_length
+ * :429-453), pcap_rw_read's end rules (pcap_rw.c:38-55: a short header or
+ * body, caplen 0 or above the 1 MiB buffer end the replay) and
+ * pcap_pkthdr_to_tpacket_hdr (:594-709) into a frame_map zeroed once
+ * (netsniff-ng.c:672).  Fills up to max records' fh / sll / caplen (each may
+ * be NULL); returns the records, or -1 for a file read_pcap refuses. */
+long nsor_pcap_meta(const char *path, nsd_frame_hdr_t *fh, nsd_sll_t *sll, uint32_t *caplen, uint32_t max)
+{
+	FILE *f = fopen(path, "rb");
+	uint8_t h[24], r[32];
+	uint32_t magic, lt, m;
+	uint16_t vmaj, vmin;
+	int swapped = 0, ll = 0, hdrsize = 16, usec;
+	nsd_sll_t s;
+	long n = 0;
+
+	if (!f)
+		return -1;
+	if (fread(h, 1, 24, f) != 24) {
+		fclose(f);
+		return -1;
+	}
+	memcpy(&magic, h, 4);
+	memcpy(&vmaj, h + 4, 2);
+	memcpy(&vmin, h + 6, 2);
+	memcpy(&lt, h + 20, 4);
+	m = magic;
+	if (m == 0xd4c3b2a1u || m == 0x4d3cb2a1u || m == 0x34cdb2a1u || m == 0x12cbe2a1u) {
+		swapped = 1;
+		m = __builtin_bswap32(m);
+	}
+	if ((m != 0xa1b2c3d4u && m != 0xa1b23c4du && m != 0xa1b2cd34u && m != 0xa1e2cb12u) ||
+	    (vmaj != 2 && __builtin_bswap16(vmaj) != 2) || (vmin != 4 && __builtin_bswap16(vmin) != 4)) {
+		fclose(f);
+		return -1;
+	}
+	if (swapped)
+		lt = __builtin_bswap32(lt);
+	if ((lt == 113 || lt == 253) && (m == 0xa1b2c3d4u || m == 0xa1b23c4du)) {
+		ll = 1;
+		hdrsize = 32;
+	}
+	if (m == 0xa1b2cd34u || m == 0xa1e2cb12u)
+		hdrsize = 24;
+	usec = m == 0xa1b2c3d4u || m == 0xa1b2cd34u;
+	memset(&s, 0, sizeof(s));
+	while ((uint32_t)n < max) {
+		uint32_t v[4], cl;
+		int k;
+		if (fread(r, 1, hdrsize, f) != (size_t)hdrsize)
+			break;
+		memcpy(v, r, 16);
+		for (k = 0; k < 4; k++)
+			if (swapped)
+				v[k] = __builtin_bswap32(v[k]);
+		cl = v[2] - (ll ? 16 : 0);
+		if (cl == 0 || cl > (1u << 20))
+			break;
+		if (fseek(f, cl, SEEK_CUR) != 0)
+			break;
+		{
+			/* a body cut short by the end of the file ends the replay */
+			long pos = ftell(f), end;
+			fseek(f, 0, SEEK_END);
+			end = ftell(f);
+			if (pos > end)
+				break;
+			fseek(f, pos, SEEK_SET);
+		}
+		if (fh) {
+			memset(&fh[n], 0, sizeof(fh[n]));
+			fh[n].sec = v[0];
+			fh[n].nsec = usec ? v[1] * 1000u : v[1];
+			fh[n].len = v[3] - (ll ? 16 : 0);
+		}
+		if (ll) {                                     /* ll_to_sockaddr :182-191 */
+			s.pkttype = (uint8_t)(r[16] << 8 | r[17]);
+			s.hatype = (uint16_t)(r[18] << 8 | r[19]);
+			s.halen = (uint8_t)(r[20] << 8 | r[21]);
+			memcpy(s.addr, r + 22, 8);
+			memcpy(&s.protocol, r + 30, 2);
+		} else if (m == 0xa1b2cd34u) {                /* struct pcap_pkthdr_kuz */
+			uint32_t ifi;
+			uint16_t pr;
+			memcpy(&ifi, r + 16, 4);
+			memcpy(&pr, r + 20, 2);
+			s.ifindex = (int32_t)(swapped ? __builtin_bswap32(ifi) : ifi);
+			s.protocol = swapped ? __builtin_bswap16(pr) : pr;
+			s.pkttype = r[22];
+		} else if (m == 0xa1e2cb12u) {                /* struct pcap_pkthdr_bkm */
+			uint16_t ifi, pr;
+			memcpy(&ifi, r + 18, 2);
+			memcpy(&pr, r + 20, 2);
+			s.ifindex = swapped ? __builtin_bswap16(ifi) : ifi;
+			s.protocol = swapped ? __builtin_bswap16(pr) : pr;
+			s.hatype = r[22];
+			s.pkttype = r[23];
+		}
+		if (sll)
+			sll[n] = s;
+		if (caplen)
+			caplen[n] = cl;
+		n++;
+	}
+	fclose(f);
+	return n;
+}
+
 typedef struct {
 	const uint8_t *frames;
 	const nsd_desc_t *desc;
+	const nsd_frame_hdr_t *fh;
+	const nsd_sll_t *sll;
+	uint64_t first_count;
 	uint32_t lo, hi;
 	int linktype, mode;
 	nsd_rec *rec;
@@ -2042,6 +2235,11 @@ static void *mt_text_worker(void *arg)
 	nsor_text_init(&t);
 	for (uint32_t i = j->lo; i < j->hi; i++) {
 		uint64_t d = j->desc[i];
+		const nsd_sll_t *sl = j->sll ? j->sll + i : NULL;
+		if (j->fh)
+			nsor_frame_hdr(j->fh + i, sl, j->frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), j->linktype,
+				       j->mode, j->first_count + i, &t);
+		g_sll = sl;
 		nsor_dissect(j->frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), j->linktype, j->mode, &t,
 			     NULL, &in);
 		j->text_bytes += t.len;
@@ -2054,6 +2252,13 @@ static void *mt_text_worker(void *arg)
 
 uint64_t nsor_dissect_batch_text_mt(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
 				    int linktype, int mode, int nthreads, uint64_t *text_bytes)
+{
+	return nsor_dissect_batch_text_fh_mt(frames, desc, NULL, NULL, 0, n, linktype, mode, nthreads, text_bytes);
+}
+
+uint64_t nsor_dissect_batch_text_fh_mt(const uint8_t *frames, const nsd_desc_t *desc, const nsd_frame_hdr_t *fh,
+				       const nsd_sll_t *sll, uint64_t first_count, uint32_t n, int linktype,
+				       int mode, int nthreads, uint64_t *text_bytes)
 {
 	pthread_t th[256];
 	mt_job *jobs;
@@ -2069,6 +2274,9 @@ uint64_t nsor_dissect_batch_text_mt(const uint8_t *frames, const nsd_desc_t *des
 		jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
 		jobs[t].linktype = linktype;
 		jobs[t].mode = mode;
+		jobs[t].fh = fh;
+		jobs[t].sll = sll;
+		jobs[t].first_count = first_count;
 		pthread_create(&th[t], NULL, mt_text_worker, &jobs[t]);
 	}
 	for (int t = 0; t < nthreads; t++) {

@@ -83,6 +83,21 @@ uint64_t nsor_dissect_batch_mt(const uint8_t *frames, const nsd_desc_t *desc, ui
 uint64_t nsor_dissect_batch_text_mt(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
 				    int linktype, int mode, int nthreads, uint64_t *text_bytes);
 
+/* The same with each packet's frame header line in front of its text
+ * (fh / sll per packet, counter first_count + i; fh NULL: none). */
+uint64_t nsor_dissect_batch_text_fh_mt(const uint8_t *frames, const nsd_desc_t *desc, const nsd_frame_hdr_t *fh,
+				       const nsd_sll_t *sll, uint64_t first_count, uint32_t n, int linktype,
+				       int mode, int nthreads, uint64_t *text_bytes);
+
+/* show_frame_hdr (dissector.h:31-116) restated: the line for one packet. */
+void nsor_frame_hdr(const nsd_frame_hdr_t *fh, const nsd_sll_t *sll, const uint8_t *pkt, uint32_t caplen,
+		    int linktype, int mode, uint64_t count, nsor_text *t);
+
+/* read_pcap's record loop restated (pcap_io.h / pcap_rw.c): each record's
+ * frame header fields, sockaddr_ll and caplen (any may be NULL) for up to
+ * max records; returns the records, -1 for a refused file. */
+long nsor_pcap_meta(const char *path, nsd_frame_hdr_t *fh, nsd_sll_t *sll, uint32_t *caplen, uint32_t max);
+
 /* Name tables (lookup.c:33-95 restated).  dir NULL => clear (names off). */
 int  nsor_lookup_init(const char *dir);
 void nsor_lookup_clear(void);

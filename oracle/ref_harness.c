@@ -21,10 +21,29 @@
  *     therefore run the oracle restatement (nsd_oracle.c) and are NOT pinned
  *     by this harness.
  *
- * Usage: nsref [-m mode] [-n confdir] [-w cols] [-i index_out] file.pcap
+ *   - the LINKTYPE_LINUX_SLL head (-f / -F only), restating
+ *     dissector_sll.c:17-63 (dissector.h -> ring.h -> config.h) over the
+ *     reference's own device_type2str / device_addr2str (dev.c) and
+ *     pcap_devtype_to_linktype (pcap_io.h, included as it lies);
+ *   - show_frame_hdr / __show_frame_hdr (dissector.h:31-116, same reason),
+ *     restated below and fed by the reference's own pcap code.
+ *
+ * With -f / -F the record loop is read_pcap's (netsniff-ng.c:659-737) over
+ * the REFERENCE's pcap objects: pcap_rw_ops (pcap_rw.c, the `-c` reader:
+ * pcap_generic_pull_fhdr -> pcap_validate_header incl. the *_LL remap,
+ * pcap_rw_read), pcap_get_length and pcap_pkthdr_to_tpacket_hdr
+ * (pcap_io.h:322-347, 594-709) into a zeroed struct frame_map, the packet
+ * counter, then show_frame_hdr and the dissector.  (The default reader, SG,
+ * reads the same records for files below its 12 MiB of iovecs.)
+ *
+ * Usage: nsref [-m mode] [-n] [-w cols] [-i index_out] [-f|-F] file.pcap
  *   -w 0    : stdin from /dev/null -> tprintf wraps at DEFAULT_TTY_SIZE (80)
  *   -w N>0  : stdin is a pty N columns wide (N=65535: effectively unwrapped)
  *   -i F    : write one u64 stdout byte offset per packet boundary to F
+ *   -f      : `netsniff-ng --in file.pcap`: frame header line + dissector
+ *   -F      : frame header lines only (no dissector; any link type)
+ * Without -f / -F every record (zero-length ones too) goes to the entry
+ * point alone, the per-packet surface the entry-point tests pin.
  * Bytes past caplen are zero (parity domain).
  */
 #define _GNU_SOURCE
@@ -37,6 +56,7 @@
 #include <sys/ioctl.h>
 #include <termios.h>
 #include <unistd.h>
+#include <arpa/inet.h>
 
 #include "hash.h"
 #include "proto.h"
@@ -45,7 +65,12 @@
 #include "tprintf.h"
 #include "lookup.h"
 
+#include "pcap_io.h"
+
 #include "nsd_oracle.h"
+
+/* as dissector.h:29 declares it (net/if.h and linux/if.h do not mix) */
+extern char *if_indextoname(unsigned ifindex, char *ifname);
 
 /* dev.c (compiles from the reference as it lies): the tables the SLL head
  * prints through (dissector_sll.c:48-51) */
@@ -78,6 +103,7 @@ struct hash_table eth_lay3;
 
 static int g_mode;
 static uint32_t g_caplen;
+static struct protocol sll_ops_h;   /* the SLL head, below */
 
 /* dissector.c:22-41 */
 int dissector_set_print_type(void *ptr, int type)
@@ -181,6 +207,7 @@ static void init_tables(int type)
 	for_each_hash_int(&eth_lay3, dissector_set_print_type, type);
 
 	dissector_set_print_type(&none_ops, type);
+	dissector_set_print_type(&sll_ops_h, type);
 }
 
 /* ---- chain loop + entry: dissector.c:43-122 (Ethernet link type) -------- */
@@ -201,7 +228,64 @@ static void dissector_main(struct pkt_buff *pkt, struct protocol *start, struct 
 		end->process(pkt);
 }
 
-static void entry(uint8_t *packet, size_t len, int linktype, int mode)
+/* ---- LINKTYPE_LINUX_SLL head: dissector_sll.c:17-63 --------------------- */
+static char *pkt_type2str(uint8_t pkttype)
+{
+	switch (pkttype) {
+	case PACKET_HOST: return "host";
+	case PACKET_BROADCAST: return "broadcast";
+	case PACKET_MULTICAST: return "multicast";
+	case PACKET_OTHERHOST: return "other host";
+	case PACKET_OUTGOING: return "outgoing";
+	case PACKET_USER: return "user";
+	case PACKET_KERNEL: return "kernel";
+	}
+	return "Unknown";
+}
+
+static int g_sll_unsupported;
+
+static void sll_print_full(struct pkt_buff *pkt)
+{
+	struct sockaddr_ll *sll = pkt->sll;
+	char addr_str[40] = {};
+
+	tprintf(" [ Linux \"cooked\"");
+	tprintf(" Pkt Type %d (%s)", sll->sll_pkttype, pkt_type2str(sll->sll_pkttype));
+	tprintf(", If Type %d (%s)", sll->sll_hatype, device_type2str(sll->sll_hatype));
+	tprintf(", Addr Len %d", sll->sll_halen);
+	tprintf(", Src (%s)", device_addr2str(sll->sll_addr, sll->sll_halen, sll->sll_hatype,
+					       addr_str, sizeof(addr_str)));
+	tprintf(", Proto 0x%x", ntohs(sll->sll_protocol));
+	tprintf(" ]\n");
+	switch (pcap_devtype_to_linktype(sll->sll_hatype)) {
+	case LINKTYPE_EN10MB:
+		pkt_set_dissector(pkt, &eth_lay2, ntohs(sll->sll_protocol));
+		break;
+	case LINKTYPE_NETLINK:
+		g_sll_unsupported = 1;   /* dissector_netlink (libnl, config.h): not built here */
+		break;
+	default:
+		tprintf(" [ Unknown protocol ]\n");
+	}
+}
+
+static void sll_print_less(struct pkt_buff *pkt)
+{
+	struct sockaddr_ll *sll = pkt->sll;
+	char addr_str[40] = {};
+
+	tprintf(" Pkt Type %d (%s)", sll->sll_pkttype, pkt_type2str(sll->sll_pkttype));
+	tprintf(", If Type %d (%s)", sll->sll_hatype, device_type2str(sll->sll_hatype));
+	tprintf(", Addr Len %d", sll->sll_halen);
+	tprintf(", Src (%s)", device_addr2str(sll->sll_addr, sll->sll_halen, sll->sll_hatype,
+					       addr_str, sizeof(addr_str)));
+	tprintf(", Proto 0x%x", ntohs(sll->sll_protocol));
+}
+
+static struct protocol sll_ops_h = { .key = 0, .print_full = sll_print_full, .print_less = sll_print_less };
+
+static void entry(uint8_t *packet, size_t len, int linktype, int mode, struct sockaddr_ll *sll)
 {
 	struct pkt_buff *pkt;
 
@@ -209,9 +293,11 @@ static void entry(uint8_t *packet, size_t len, int linktype, int mode)
 		return;
 	pkt = pkt_alloc(packet, len);
 	pkt->link_type = linktype;
-	pkt->sll = NULL;
+	pkt->sll = sll;
 	if (linktype == 1 || (uint32_t)linktype == 0x01000000u)
 		dissector_main(pkt, &ethernet_ops, &none_ops);
+	else if (sll && (linktype == LINKTYPE_LINUX_SLL || (uint32_t)linktype == 0x71000000u))
+		dissector_main(pkt, &sll_ops_h, &none_ops);
 	else
 		dissector_main(pkt, &none_ops, NULL);
 	switch (mode) {
@@ -245,9 +331,132 @@ static int setup_stdin(int cols)
 
 static uint32_t sw32(uint32_t v, int swap) { return swap ? __builtin_bswap32(v) : v; }
 
+/* ---- show_frame_hdr: dissector.h:31-116 (+ ring.h:34-84 helpers) ----------
+ * Only the TPACKET_V2 form read_pcap uses (v3 false, raw_hdr = the zeroed
+ * frame_map's tp_h).  ring.h is built with HAVE_TPACKET3 (configure:334-360
+ * finds it on any kernel with tpacket_v3), so tpacket_has_vlan_info reads
+ * the status through the tpacket3_hdr view of this tpacket2_hdr
+ * (tpacket_uhdr(*hdr, tp_status, true), ring.h:83): offset 20, which in a
+ * tpacket2_hdr is tp_nsec; the VLAN tci / tpid helpers return 0 for v2. */
+static const char *const packet_types[256] = {
+	[PACKET_HOST] = "<", [PACKET_BROADCAST] = "B", [PACKET_MULTICAST] = "M",
+	[PACKET_OTHERHOST] = "P", [PACKET_OUTGOING] = ">", [PACKET_USER] = "K->U",
+	[PACKET_KERNEL] = "U->K",
+};
+
+static const char *show_ts_source(uint32_t status)
+{
+	if (status & TP_STATUS_TS_RAW_HARDWARE)
+		return "(raw hw ts)";
+	else if (status & TP_STATUS_TS_SYS_HARDWARE)
+		return "(sys hw ts)";
+	else if (status & TP_STATUS_TS_SOFTWARE)
+		return "(sw ts)";
+	return "";
+}
+
+static void show_frame_hdr_v2(uint8_t *packet, size_t len, int linktype, struct sockaddr_ll *s_ll,
+			      struct tpacket2_hdr *h2, int mode, unsigned long count)
+{
+	char tmp[IFNAMSIZ];
+	uint8_t pkttype = s_ll->sll_pkttype;
+	const char *ifn;
+	uint32_t st3;
+
+	if (mode == PRINT_NONE)
+		return;
+	if (linktype == LINKTYPE_NETLINK && len >= 16 && pkttype == PACKET_OUTGOING) {
+		uint32_t pid;
+		memcpy(&pid, packet + 12, 4);   /* struct nlmsghdr.nlmsg_pid */
+		pkttype = pid == 0 ? PACKET_KERNEL : PACKET_USER;
+	}
+	ifn = if_indextoname(s_ll->sll_ifindex, tmp);
+	switch (mode) {
+	case PRINT_LESS:
+		tprintf("%s %s %u #%lu", packet_types[pkttype] ? : "?", ifn ? : "?", h2->tp_len, count);
+		break;
+	default:
+		tprintf("%s %s %u %us.%uns #%lu %s\n", packet_types[pkttype] ? : "?", ifn ? : "?",
+			h2->tp_len, h2->tp_sec, h2->tp_nsec, count, show_ts_source(h2->tp_status));
+		st3 = ((struct tpacket3_hdr *)(void *)h2)->tp_status;
+		if (st3 & (TP_STATUS_VLAN_VALID | TP_STATUS_VLAN_TPID_VALID)) {
+			uint16_t tci = 0;
+			tprintf(" [ tpacketv3 VLAN ");
+			tprintf("Prio (%u), ", (tci & 0xe000) >> 13);
+			tprintf("CFI (%u), ", (tci & 0x1000) >> 12);
+			tprintf("ID (%u), ", tci & 0x0fff);
+			tprintf("Proto (0x%.4x)", 0);
+			tprintf(" ]\n");
+		}
+		break;
+	}
+}
+
+/* struct frame_map (ring.h:86-89; ring.h needs config.h) */
+struct frame_map {
+	struct tpacket2_hdr tp_h;
+	struct sockaddr_ll s_ll;
+};
+
+/* read_pcap's loop (netsniff-ng.c:659-737) over the reference's RW reader */
+static int replay(const char *path, int mode, int frames_only, FILE *fi)
+{
+	const struct pcap_file_ops *io = &pcap_rw_ops;
+	uint32_t magic, link_type;
+	unsigned long count = 0;
+	pcap_pkthdr_t phdr;
+	struct frame_map fm;
+	size_t out_len = 1 << 20, hw = 0;
+	uint8_t *out;
+	int fd, ret;
+
+	fd = open(path, O_RDONLY);
+	if (fd < 0)
+		return 1;
+	if (io->pull_fhdr_pcap(fd, &magic, &link_type))
+		return 1;
+	memset(&fm, 0, sizeof(fm));
+	out = calloc(1, out_len + 4096);
+	for (;;) {
+		uint32_t caplen;
+		uint64_t pos;
+
+		ret = io->read_pcap(fd, &phdr, magic, out, out_len);
+		if (ret < 0)
+			break;
+		caplen = pcap_get_length(&phdr, magic);
+		if (caplen == 0)
+			continue;   /* unreachable: the reader returns -EINVAL first */
+		/* parity domain: bytes past caplen read as zero */
+		if (hw > caplen)
+			memset(out + caplen, 0, hw - caplen);
+		hw = caplen;
+		pcap_pkthdr_to_tpacket_hdr(&phdr, magic, &fm.tp_h, &fm.s_ll);
+		count++;
+		show_frame_hdr_v2(out, fm.tp_h.tp_snaplen, link_type, &fm.s_ll, &fm.tp_h, mode, count);
+		if (!frames_only) {
+			g_caplen = fm.tp_h.tp_snaplen;
+			entry(out, fm.tp_h.tp_snaplen, (int)link_type, mode, &fm.s_ll);
+			if (g_sll_unsupported)
+				return 3;
+		} else {
+			tprintf_flush();
+		}
+		if (fi) {
+			fflush(stdout);
+			pos = (uint64_t)ftello(stdout);
+			fwrite(&pos, 8, 1, fi);
+		}
+	}
+	fflush(stdout);
+	close(fd);
+	free(out);
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
-	int opt, cols = 0, names = 0;
+	int opt, cols = 0, names = 0, fh_mode = 0;
 	const char *index_out = NULL;
 	FILE *f, *fi = NULL;
 	uint32_t fh[6];
@@ -258,8 +467,10 @@ int main(int argc, char **argv)
 	g_mode = PRINT_NORM;
 	if (argc > 1 && !strcmp(argv[1], "-T"))
 		return dump_dev_tables();
-	while ((opt = getopt(argc, argv, "m:nw:i:")) != -1) {
+	while ((opt = getopt(argc, argv, "m:nw:i:fF")) != -1) {
 		switch (opt) {
+		case 'f': fh_mode = 1; break;
+		case 'F': fh_mode = 2; break;
 		case 'm': g_mode = atoi(optarg); break;
 		case 'n': names = 1; break;
 		case 'w': cols = atoi(optarg); break;
@@ -288,6 +499,16 @@ int main(int argc, char **argv)
 	}
 	init_tables(g_mode);
 
+	if (fh_mode) {
+		int rc;
+		if (index_out)
+			fi = fopen(index_out, "wb");
+		rc = replay(argv[optind], g_mode, fh_mode == 2, fi);
+		if (fi)
+			fclose(fi);
+		return rc;
+	}
+
 	f = fopen(argv[optind], "rb");
 	if (!f || fread(fh, 4, 6, f) != 6) {
 		fprintf(stderr, "cannot read %s\n", argv[optind]);
@@ -310,7 +531,7 @@ int main(int argc, char **argv)
 		if (fread(buf, 1, caplen, f) != caplen)
 			break;
 		g_caplen = caplen;
-		entry(buf, caplen, (int)sw32(fh[5], swap), g_mode);
+		entry(buf, caplen, (int)sw32(fh[5], swap), g_mode, NULL);
 		if (fi) {
 			fflush(stdout);
 			pos = (uint64_t)ftello(stdout);

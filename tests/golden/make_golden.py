@@ -17,7 +17,20 @@
                        C2/C3/C4 (NORM, LESS) and of the oracle records / counters
   wsum.json            sum of W(pkt) (algorithmic read bytes) over
                        the 16M-packet shards used by bench.py
+  ip_vectors.npz       tests/ip_vectors.py: IPv4 / IPv6 / ICMPv4 frames and
+                       the values the reference's csum.h / ipv4.h / ipv6.h
+                       give for them (oracle/_ref/libnsdrefip.so; --ip-only)
   (--edge-only: the two pcaps and their texts only)
+  <pcap>.fh.m<M>.w<C>  `netsniff-ng --in <pcap>` (nsref -f: read_pcap's loop
+                       over the reference's own pcap reader and
+                       pcap_pkthdr_to_tpacket_hdr, show_frame_hdr's line
+                       before each packet's dissector text) for tiny, big,
+                       leaves and the record-format fixtures below
+  fh_*.pcap            edge.pcap's non-empty frames in each record format
+                       (tests/pcap_formats.py: usec / nsec / Kuznetzov /
+                       Borkmann, both byte orders, the *_LL form of SLL
+                       files) with varied timestamps, lengths and link-layer
+                       metadata (--fh-only: these and the .fh. texts only)
 
 IPv4/IPv6 layers inside nsref come from the restatement (their reference
 sources need the configure-generated config.h); see oracle/ref_harness.c.
@@ -102,8 +115,41 @@ def big_cases():
     return [tiny[0], udp_big, edge[5], icmp_big, v6, tiny[1]]
 
 
+def frame_goldens():
+    """The `--in` texts with frame headers (nsref -f)."""
+    import pcap_formats as PF
+    _, edge = T.read_pcap(os.path.join(HERE, "edge.pcap"))
+    frames = [p for p in edge if p]
+    for name, kw in PF.VARIANTS.items():
+        path = os.path.join(HERE, name + ".pcap")
+        PF.write(path, frames, **kw)
+        modes = MODES if name == "fh_usec" else (T.PRINT_NORM, T.PRINT_LESS)
+        for m in modes:
+            save_text(os.path.join(HERE, f"{name}.fh.m{m}.w65535"), T.run_ref(path, mode=m, cols=65535, frames="f"))
+        if name in ("fh_usec", "fh_kuz"):
+            for m in (T.PRINT_NORM, T.PRINT_LESS):
+                save_text(os.path.join(HERE, f"{name}.fh.m{m}.w80"), T.run_ref(path, mode=m, cols=0, frames="f"))
+    for stem, modes in (("tiny", MODES), ("big", MODES), ("leaves", (T.PRINT_NORM, T.PRINT_LESS))):
+        path = os.path.join(HERE, stem + ".pcap")
+        for m in modes:
+            save_text(os.path.join(HERE, f"{stem}.fh.m{m}.w65535"), T.run_ref(path, mode=m, cols=65535, frames="f"))
+    for m in (T.PRINT_NORM, T.PRINT_LESS):
+        save_text(os.path.join(HERE, f"tiny.fh.m{m}.w80"), T.run_ref(os.path.join(HERE, "tiny.pcap"), mode=m,
+                                                                     cols=0, frames="f"))
+
+
 def main():
     T.build_native()
+    if "--fh-only" in sys.argv:
+        frame_goldens()
+        return
+    if "--prefix-only" in sys.argv:
+        prefix_digests()
+        return
+    import ip_vectors
+    ip_vectors.save()
+    if "--ip-only" in sys.argv:
+        return
     leaves = os.path.join(HERE, "leaves.pcap")
     T.write_pcap(leaves, leaf_cases.cases())
     for m in (T.PRINT_NORM, T.PRINT_LESS):
@@ -127,9 +173,16 @@ def main():
         for m in (T.PRINT_NORM, T.PRINT_LESS):
             save_text(f"{stem}.m{m}.w80", T.run_ref(pcap, mode=m, cols=0))
             save_text(f"{stem}.names.m{m}.w65535", T.run_ref(pcap, mode=m, cols=65535, names=True))
+    frame_goldens()
     if "--edge-only" in sys.argv:
         return
+    prefix_digests()
+    if "--prefix-only" in sys.argv:
+        return
+    wsum_shards()
 
+
+def prefix_digests():
     prefix = {}
     for key, cfg in (("udp64", T.SYN_UDP64), ("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):
         path = f"/tmp/golden_{key}.pcap"
@@ -137,14 +190,18 @@ def main():
         frames, desc = T.make_batch(cfg, 65536)
         for m in (T.PRINT_NORM, T.PRINT_LESS):
             txt = b"".join(T.run_ref(path, mode=m, cols=65535, timeout=600))
+            txt_fh = b"".join(T.run_ref(path, mode=m, cols=65535, timeout=600, frames="f"))
             rec, ext, cnt, sw = T.oracle_records(frames, desc, mode=m)
             prefix[f"{key}:m{m}"] = {"text_sha256": hashlib.sha256(txt).hexdigest(),
+                                     "replay_text_sha256": hashlib.sha256(txt_fh).hexdigest(),
                                      "records_sha256": rec_digest(rec, ext),
                                      "counters": [int(x) for x in cnt], "wsum": sw}
         os.unlink(path)
     with open(os.path.join(HERE, "prefix.json"), "w") as f:
         json.dump(prefix, f, indent=1)
 
+
+def wsum_shards():
     wsum = {}
     n = 1 << 24
     for key, cfg, shards in (("imix", T.SYN_IMIX, 8), ("ipv6x", T.SYN_IPV6X, 1)):

@@ -191,6 +191,16 @@ def oracle():
         lib.nsor_text_free.argtypes = [ctypes.POINTER(_Text)]
         lib.nsor_lookup_init.restype = ctypes.c_int
         lib.nsor_lookup_init.argtypes = [ctypes.c_char_p]
+        lib.nsor_dissect_batch_text_fh_mt.restype = ctypes.c_uint64
+        lib.nsor_dissect_batch_text_fh_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        lib.nsor_frame_hdr.restype = None
+        lib.nsor_frame_hdr.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(_Text)]
+        lib.nsor_pcap_meta.restype = ctypes.c_long
+        lib.nsor_pcap_meta.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint32]
         _oracle = lib
     return _oracle
 
@@ -229,12 +239,50 @@ def oracle_text_packets(frames, desc, linktype=1, mode=PRINT_NORM, sll=None):
     return out
 
 
-def run_ref(pcap_path, mode=PRINT_NORM, cols=65535, names=False, timeout=120):
-    """Run oracle/_ref/nsref; returns list of per-packet text (bytes)."""
+# nsd_frame_hdr_t / struct sockaddr_ll (as netsniff-ng_amd/nsd.py declares them)
+FH_DTYPE = np.dtype([("len", "<u4"), ("sec", "<u4"), ("nsec", "<u4"), ("status", "<u4"), ("vlan_tci", "<u4"),
+                     ("vlan_tpid", "<u2"), ("v3", "u1"), ("reserved", "u1")])
+SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
+                      ("pkttype", "u1"), ("halen", "u1"), ("addr", "u1", (8,))])
+
+
+def oracle_pcap_meta(path, max_n=1 << 20):
+    """read_pcap's per-record frame header fields, sockaddr_ll and caplen,
+    restated (nsor_pcap_meta): (fh, sll, caplen) arrays, or None for a file
+    read_pcap refuses."""
+    fh = np.zeros(max_n, dtype=FH_DTYPE)
+    sll = np.zeros(max_n, dtype=SLL_DTYPE)
+    cl = np.zeros(max_n, dtype=np.uint32)
+    n = oracle().nsor_pcap_meta(os.fsencode(path), fh.ctypes.data, sll.ctypes.data, cl.ctypes.data, max_n)
+    if n < 0:
+        return None
+    return fh[:n], sll[:n], cl[:n]
+
+
+def oracle_frame_hdr(fh, sll=None, pkt=b"", linktype=1, mode=PRINT_NORM, count=1):
+    """show_frame_hdr's line restated (nsor_frame_hdr)."""
+    lib = oracle()
+    f = np.asarray(fh, dtype=FH_DTYPE).reshape(1)
+    s = None if sll is None else np.asarray(sll, dtype=SLL_DTYPE).reshape(1)
+    p = np.frombuffer(bytes(pkt) + b"\0", dtype=np.uint8)
+    t = _Text()
+    lib.nsor_frame_hdr(f.ctypes.data, None if s is None else s.ctypes.data, p.ctypes.data, len(pkt), linktype,
+                       mode, count, ctypes.byref(t))
+    out = ctypes.string_at(t.buf, t.len) if t.len else b""
+    lib.nsor_text_free(ctypes.byref(t))
+    return out
+
+
+def run_ref(pcap_path, mode=PRINT_NORM, cols=65535, names=False, timeout=120, frames=None):
+    """Run oracle/_ref/nsref; returns list of per-packet text (bytes).
+    frames="f": `netsniff-ng --in` (frame header line + dissector, read_pcap's
+    loop over the reference's pcap reader); "F": frame header lines only."""
     idx = pcap_path + f".m{mode}.idx"
     args = [REF_BIN, "-m", str(mode), "-w", str(cols), "-i", idx]
     if names:
         args.append("-n")
+    if frames:
+        args.append("-" + frames)
     args.append(pcap_path)
     txt = pcap_path + f".m{mode}.txt"
     with open(txt, "wb") as fo:

@@ -14,6 +14,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -51,6 +52,47 @@ def test_bench_rank_body(tmp_path):
         _, _, want, _ = T.oracle_records(frames, desc)
         assert np.array_equal(got, want * np.uint64(steps))
         assert int(got[32]) == world * per_rank * steps
+
+
+def _dev_worker(rank, world, port, key, per_rank, steps, out):
+    """One rank of the device branch: both ranks on cuda:0 (one GPU box),
+    gloo over CUDA tensors (RCCL refuses two ranks on one device)."""
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"], os.environ["WORLD_SIZE"], os.environ["LOCAL_RANK"] = str(rank), str(world), str(rank)
+    sys.path.insert(0, ROOT)
+    import bench
+    torch.cuda.set_device(0)
+    nsd_dist.init("gloo")
+    r, w, _ = nsd_dist.rank_env()
+    args = bench.parse_args(["--gpus", str(w), "--config", key, "--packets", str(per_rank), "--steps", str(steps),
+                             "--warmup", "1"])
+    b, m = bench.measure_rank(args, r, w, torch.device("cuda", 0), engine="device")
+    assert b.counters.is_cuda and m["accumulate"]
+    if r == 0:
+        np.save(out, np.concatenate([m["counters"].view(np.int64), [m["total_pkts"]], [m["kern_ms"] > 0]]))
+    b.free()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key,cfg", [("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)])
+def test_bench_rank_body_device(tmp_path, key, cfg):
+    """bench.measure_rank's device branch with world size 2: each rank's
+    shard resident on the GPU and walked by the kernels, all_ranks_agree /
+    reduce_counters / max_over_ranks on device tensors (the reference scales
+    out by processes too: PACKET_FANOUT, ring_rx.c:197-215).  The summed
+    counters equal the oracle's over both shards x the steps."""
+    world, per_rank, steps = 2, 1 << 16, 3
+    out = str(tmp_path / f"{key}.npy")
+    mp.spawn(_dev_worker, args=(world, nsd_dist.free_port(), key, per_rank, steps, out), nprocs=world, join=True)
+    res = np.load(out)
+    got, total, timed = res[:-2].view(np.uint64), int(res[-2]), int(res[-1])
+    assert total == world * per_rank and timed == 1
+    frames, desc = T.make_batch(cfg, world * per_rank)
+    _, _, want, _ = T.oracle_records(frames, desc)
+    assert np.array_equal(got, want * np.uint64(steps))
 
 
 def test_spawn_refuses_missing_gpus():

@@ -144,32 +144,33 @@ def replayable(name, mode, tmp_path):
     return path, keep
 
 
+def frame_lines(path, mode, accepted=None):
+    """show_frame_hdr's line per replayed record (restated, pinned against
+    the reference's pcap code in test_frame_hdr.py); with `accepted` (record
+    indexes a filter passes) only theirs, counted among themselves."""
+    lt = nsd.pcap_frame_hdrs(path)[0]
+    fh, sll, _ = T.oracle_pcap_meta(path)
+    _, pkts, _, _ = nsd.pcap_frame_hdrs(path)
+    idx = range(len(fh)) if accepted is None else accepted
+    return [T.oracle_frame_hdr(fh[i], sll[i], pkts[i], linktype=lt, mode=mode, count=k + 1)
+            for k, i in enumerate(idx)]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["tiny", "edge", "big"])
 @pytest.mark.parametrize("mode", MODES)
-def test_replay_matches_golden(tmp_path, name, mode):
-    """`--in file.pcap` end to end on the device == the reference's text."""
-    gold = TG.load_golden(f"{name}.m{mode}.w65535")
-    path, keep = replayable(name, mode, tmp_path)
-    if name == "tiny":
-        assert len(keep) == 1000
+def test_replay_edge_matches_golden(tmp_path, mode):
+    """`--in edge.pcap` end to end on the device: every record's frame header
+    line, then the text the reference's parser objects print for it
+    (tiny / big / leaves / the record-format fixtures: test_frame_hdr.py,
+    whole texts of the reference's read_pcap loop)."""
+    gold = TG.load_golden(f"edge.m{mode}.w65535")
+    path, keep = replayable("edge", mode, tmp_path)
     cnt = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
-    n, text = nsd.replay_pcap(path, mode=mode, counters=cnt, threads=1 if name == "edge" else 4, cols=65535)
+    n, text = nsd.replay_pcap(path, mode=mode, counters=cnt, threads=1, cols=65535)
     assert n == len(keep)
-    assert text == b"".join(gold[i] for i in keep)
+    fl = frame_lines(path, mode)
+    assert text == b"".join(fl[k] + gold[i] for k, i in enumerate(keep))
     assert int(cnt[nsd.CNT_PKTS]) == len(keep)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
-def test_replay_leaves_match_golden(tmp_path, mode):
-    """The leaf frames end to end: device records (leaf end cursors from the
-    device walk) -> host text == the reference's."""
-    gold = TG.load_golden(f"leaves.m{mode}.w65535")
-    path, keep = replayable("leaves", mode, tmp_path)
-    n, text = nsd.replay_pcap(path, mode=mode, threads=4, cols=65535)
-    assert n == len(keep) == len(gold)
-    assert text == b"".join(gold)
 
 
 @pytest.mark.gpu
@@ -181,9 +182,10 @@ def test_replay_wrapped_and_filtered(tmp_path, mode):
     path, keep = replayable("edge", mode, tmp_path)
     unwrapped = TG.load_golden(f"edge.m{mode}.w65535")
     n, text = nsd.replay_pcap(path, mode=mode, cols=80)
+    fl = frame_lines(path, mode)
     state, want = 0, b""
-    for i in keep:
-        w, state = nsd.tprintf_wrap(unwrapped[i], cols=80, state=state)
+    for k, i in enumerate(keep):
+        w, state = nsd.tprintf_wrap(fl[k] + unwrapped[i], cols=80, state=state)
         want += w
     assert n == len(keep) and text == want
     # bpfc.8 "IPv4 TCP" program: ldh [12]; jeq #0x800 ...; ldb [23]; jeq #6; ret #-1; ret #0
@@ -193,7 +195,9 @@ def test_replay_wrapped_and_filtered(tmp_path, mode):
     acc = [i for i in keep if len(pkts[i]) >= 24 and pkts[i][12:14] == b"\x08\x00" and pkts[i][23] == 6]
     assert acc
     n, text = nsd.replay_pcap(path, mode=mode, prog=bp)
-    assert n == len(acc) and text == b"".join(unwrapped[i] for i in acc)
+    # the packet counter counts the records the filter passes (netsniff-ng.c:723-730)
+    fl = frame_lines(path, mode, accepted=[keep.index(i) for i in acc])
+    assert n == len(acc) and text == b"".join(fl[k] + unwrapped[i] for k, i in enumerate(acc))
 
 
 @pytest.mark.gpu
@@ -202,11 +206,12 @@ def test_replay_wrapped_and_filtered(tmp_path, mode):
 def test_replay_prefix_digest(tmp_path, key, cfg, mode):
     """64K-packet synthetic pcaps (C2/C3/C4 prefixes) replayed through the
     device with 8 formatting threads: the text's SHA-256 equals the digest of
-    the reference parser objects' text (tests/golden/prefix.json)."""
+    the reference's read_pcap loop over the same file (nsref -f: frame
+    headers + the parser objects' text; tests/golden/prefix.json)."""
     import hashlib
     import json
     with open(os.path.join(G, "prefix.json")) as f:
-        want = json.load(f)[f"{key}:m{mode}"]["text_sha256"]
+        want = json.load(f)[f"{key}:m{mode}"]["replay_text_sha256"]
     path = str(tmp_path / f"{key}.pcap")
     T.synth().nsd_synth_pcap(cfg, T.SEED, 0, 65536, path.encode())
     n, text = nsd.replay_pcap(path, mode=mode, threads=8)
@@ -284,7 +289,8 @@ def test_replay_sll_file(tmp_path, mode):
     fmt, rc = nsd.format_batch(frames, desc, orec, oext, mode=mode, linktype=nsd.LINKTYPE_LINUX_SLL,
                                sll=as_read(slls))
     assert not any(rc)
-    want = b"".join(fmt[i] if u else t for i, (t, u) in enumerate(ora))
+    fl = frame_lines(path, mode)
+    want = b"".join(fl[i] + (fmt[i] if u else t) for i, (t, u) in enumerate(ora))
     assert sum(u for _, u in ora) < len(ora) // 2
     cnt = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
     n, text = nsd.replay_pcap(path, mode=mode, counters=cnt)

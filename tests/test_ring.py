@@ -15,10 +15,11 @@ import nsd_testlib as T
 PACKET_HOST, PACKET_OUTGOING = 0, 4
 
 
-def make_block(pkts, pkttypes=None, ifindex=None, block_len=1 << 20, mac_pad=2, slls=None):
+def make_block(pkts, pkttypes=None, ifindex=None, block_len=1 << 20, mac_pad=2, slls=None, hv1=None):
     """tpacket_block_desc (48 B) + per frame tpacket3_hdr (48 B) + sockaddr_ll
     (20 B) + pad so the MAC header sits at 2 mod 16 (as the kernel places it),
-    frames TPACKET_ALIGN'ed (16)."""
+    frames TPACKET_ALIGN'ed (16).  hv1: per frame (tp_status, tp_vlan_tci,
+    tp_vlan_tpid) (default status 1, no VLAN)."""
     blk = bytearray(block_len)
     first = 48
     h = first
@@ -27,7 +28,9 @@ def make_block(pkts, pkttypes=None, ifindex=None, block_len=1 << 20, mac_pad=2, 
         mac = ((48 + 20 + 15) & ~15) + mac_pad      # TPACKET_ALIGN(hdr + sll) + NET_IP_ALIGN-ish
         nxt = (mac + len(p) + 15) & ~15
         last = i == len(pkts) - 1
-        hdr = struct.pack("<IIIIIIHH", 0 if last else nxt, 1000 + i, 7 * i, len(p), len(p) + 4, 1, mac, mac + 14)
+        st, tci, tpid = hv1[i] if hv1 else (1, 0, 0)
+        hdr = struct.pack("<IIIIIIHHIIH", 0 if last else nxt, 1000 + i, 7 * i, len(p), len(p) + 4, st, mac,
+                          mac + 14, 0x5A5A5A5A, tci, tpid)
         blk[h:h + len(hdr)] = hdr
         pt = pkttypes[i] if pkttypes else PACKET_HOST
         ix = ifindex[i] if ifindex else 2
