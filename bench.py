@@ -29,6 +29,7 @@ torch.distributed.run (one rank per GPU, weak scaling: every rank walks its
 own 16M-packet shard).  Rank 0 prints one JSON line.
 """
 import argparse
+import ctypes
 import csv
 import glob
 import hashlib
@@ -139,7 +140,7 @@ class Batch:
         if ev is not None:
             ev[1].record()
 
-    def roofline(self, kern_ms, traffic=None, copy_gbs=None):
+    def roofline(self, kern_ms, traffic=None, copy_gbs=None, ceiling=None):
         if self.wsum is None:
             return None
         read_b = DESC_B * self.n + self.wsum
@@ -157,6 +158,11 @@ class Batch:
         if copy_gbs:
             r["copy_gbs"] = round(copy_gbs, 1)
             r["frac_of_copy"] = round(achieved / copy_gbs, 4)
+        if ceiling:
+            # the achievable read rate measured in this run (read_ceiling)
+            r["read_ceiling_gbs"] = ceiling["gbs"]
+            r["read_frac_of_ceiling"] = round(read_b / (kern_ms * 1e-3) / 1e9 / ceiling["gbs"], 4)
+            r["frac_of_ceiling"] = round(achieved / ceiling["gbs"], 4)
         return r
 
     def free(self):
@@ -488,10 +494,21 @@ def bpf_bench(b, steps, warmup):
         torch.cuda.synchronize()
         res[compact] = ev[0].elapsed_time(ev[1]) / steps
     kept = int(count.item())
+    # the program's verdict restated over the resident bytes (ethertype
+    # 0x0800 at 12, protocol 6 at 23; a load past caplen returns 0,
+    # bpf.c:538-551): the accepted count the compaction wrote must match
+    d = b.desc
+    off = d & ((1 << 40) - 1)
+    cap = d >> 40
+    fr = b.frames
+    ok = (cap >= 24) & (fr[off + 12] == 8) & (fr[off + 13] == 0) & (fr[off + 23] == 6)
+    want = int(ok.sum().item())
+    assert kept == want, f"bpf: {kept} accepted, restated program {want}"
     algo = 8 * n + b.line_bytes + 4 * n
     gbs = algo / (res[False] * 1e-3) / 1e9
     bp.close()
-    return {"program": "bpfc.8 'Only allow IPv4 TCP packets' (6 insns)", "accepted": kept,
+    return {"program": "bpfc.8 'Only allow IPv4 TCP packets' (6 insns)", "workload": CONFIGS[b.key]["name"],
+            "packets": n, "accepted": kept, "accepted_check": "equal to the program restated over the bytes",
             "value": round(n / (res[False] * 1e-3) / 1e6, 1), "unit": "Mpkt/s",
             "kernel_ms": round(res[False], 4), "compact_ms": round(res[True], 4),
             "compact_mpps": round(n / (res[True] * 1e-3) / 1e6, 1),
@@ -606,6 +623,42 @@ def copy_rate(dev):
     gbs = 2 * cbuf.numel() * 5 / (ce[0].elapsed_time(ce[1]) * 1e-3) / 1e9
     del cbuf, cdst
     return gbs
+
+
+BW_SO = os.path.join(ROOT, "tools", "bw", "libnsdbw.so")
+
+
+def read_ceiling(buf, reps=5):
+    """The read rate this device reaches in this run (the
+    achievable rate beside the spec peak): tools/bw/nsd_bw.hip streams the
+    resident frame buffer of the timed batch (four 16-B loads in flight per
+    lane, grid-stride), best over 2 / 4 / 8 blocks of 256 per CU x plain /
+    nontemporal loads, `reps` launches each between HIP events.  A read-only
+    ceiling, unlike copy_gbs (read + write of a torch copy)."""
+    L = ctypes.CDLL(BW_SO)
+    L.nsd_bw_read.restype = ctypes.c_int
+    L.nsd_bw_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                              ctypes.c_void_p]
+    nbytes = (buf.numel() // 16) * 16
+    sink = torch.zeros(4, dtype=torch.int32, device=buf.device)
+    stream = torch.cuda.current_stream().cuda_stream
+    best = None
+    for bpc in (2, 4, 8):
+        for nt in (0, 1):
+            def go():
+                assert L.nsd_bw_read(buf.data_ptr(), nbytes, bpc, nt, stream, sink.data_ptr()) == 0
+            go()
+            go()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(reps):
+                go()
+            ev[1].record()
+            torch.cuda.synchronize()
+            gbs = nbytes * reps / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9
+            if best is None or gbs > best["gbs"]:
+                best = {"gbs": round(gbs, 1), "blocks_per_cu": bpc, "nontemporal": bool(nt), "bytes": nbytes}
+    return best
 
 
 def measure_rank(args, rank, world, dev, engine="device"):
@@ -734,9 +787,14 @@ def main():
     mpps = total_pkts * args.steps / elapsed / 1e6
 
     copy_gbs = copy_rate(dev)
+    ceiling = read_ceiling(b.frames)
     tr = traffic.get(args.config) if isinstance(traffic, dict) else None
-    roofline = b.roofline(kern_ms, tr, copy_gbs)
-    bpf = None if args.no_bpf or not solo else bpf_bench(b, args.steps, args.warmup)
+    roofline = b.roofline(kern_ms, tr, copy_gbs, ceiling)
+    # the BPF leg filters C3's IMIX (its "IPv4 TCP" program accepts the
+    # untagged TCP sixth; C2's UDP would leave the compaction nothing)
+    want_bpf = solo and not args.no_bpf
+    bpf = bpf_bench(b, args.steps, args.warmup) if want_bpf and (args.config == "imix" or "imix" not in legs) \
+        else None
     frame_bytes = b.frame_bytes
     b.free()
     torch.cuda.empty_cache()
@@ -748,7 +806,7 @@ def main():
         oms = time_steps(ob, args.mode, args.steps, args.warmup, 0)
         other = {"records": "full 16 B (nsd_rec)" if compact else "compact 8 B (nsd_crec)",
                  "value": round(ob.n / (oms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
-                 "roofline": ob.roofline(oms, None, copy_gbs)}
+                 "roofline": ob.roofline(oms, None, copy_gbs, ceiling)}
         ob.free()
         torch.cuda.empty_cache()
 
@@ -758,11 +816,13 @@ def main():
         ms = time_steps(lb, args.mode, args.steps, args.warmup, args.grid)
         lc = lb.counters.cpu().numpy().view(np.uint64)
         assert int(lc[nsd.CNT_PKTS]) == lb.n, f"{key}: counter check failed"
+        if key == "imix" and want_bpf and bpf is None:
+            bpf = bpf_bench(lb, args.steps, args.warmup)
         ltr = traffic.get(key) if isinstance(traffic, dict) else None
         leg_out[key] = {"workload": CONFIGS[key]["name"], "packets": lb.n, "schedule": nsd.last_schedule(),
                         "value": round(lb.n / (ms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
                         "gbps_frames": round(lb.frame_bytes / (ms * 1e-3) / 1e9, 1),
-                        "roofline": lb.roofline(ms, ltr, copy_gbs)}
+                        "roofline": lb.roofline(ms, ltr, copy_gbs, ceiling)}
         lb.free()
         torch.cuda.empty_cache()
 

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <mutex>
 
 #include "nsd_walk.h"
@@ -41,7 +42,6 @@ constexpr int WAVES = BLOCK / 64;
 // launcher to choose the schedule (split or fused, nsd_launch_dissect_rec):
 // [0] packets the fast walk handed to the general walk, [1] ICMPv4 messages
 // left to a checksum pass (longer than their window)
-__device__ unsigned long long g_sched_acc[2];
 constexpr int WIN1 = 64;         // bytes per staged window, pass 1
 #ifndef NSD_WIN2
 #define NSD_WIN2 128
@@ -60,6 +60,9 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #endif
 #ifndef NSD_LATE
 #define NSD_LATE 1                 // a walker-heavy tile's successor loads its chunks after the walkers (0: before, with L2 touches)
+#endif
+#ifndef NSD_FAST_EXT
+#define NSD_FAST_EXT 1             // the fused kernel's fast walk steps extension headers in its window
 #endif
 #ifndef NSD_CSUM_SPLIT
 #define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
@@ -98,9 +101,11 @@ struct HbmBytes {
 // with their 16-byte slots XOR-swizzled by sw); bytes outside it are not fetched, the
 // source records the miss and the walk gives the packet up to the general
 // walk.  Otherwise (the general walk's continuation windows, stage_glds): a
-// row of WIN bytes filled by LDS-DMA with its 16-byte slots XOR-swizzled
-// (dword j at j ^ sw) and nothing zeroed, so every read masks the bytes at
-// offsets >= caplen itself; bytes outside the window come from HBM.
+// row of up to WIN bytes filled by LDS-DMA with its 16-byte slots
+// XOR-swizzled (dword j at j ^ sw) and nothing zeroed, so every read masks
+// the bytes at offsets >= caplen itself; only its first wl bytes are staged
+// (a walker's window ends at a line boundary, walkers()), and bytes outside
+// them come from HBM.
 template <bool FAST, int WIN>
 struct LSrc {
 	const uint32_t *win;     // this lane's window row
@@ -112,6 +117,7 @@ struct LSrc {
 	uint32_t wb;             // aligned position of window byte 0 (multiple of 16)
 	mutable bool miss;
 	uint32_t sw;             // continuation rows: slot swizzle (dword index xor)
+	uint32_t wl = WIN;       // bytes of the row staged from wb (continuation rows; FAST: WIN)
 
 	__device__ __forceinline__ uint32_t dw(uint32_t j) const { return win[j ^ sw]; }
 	__device__ __forceinline__ int lay3(uint32_t key) const { return lay3t[key & 255]; }
@@ -146,13 +152,13 @@ struct LSrc {
 		} else {
 			if (o >= caplen)
 				return 0;
-			return r < WIN ? (uint8_t)(dw(r >> 2) >> ((r & 3) * 8)) : p[o];
+			return r < wl ? (uint8_t)(dw(r >> 2) >> ((r & 3) * 8)) : p[o];
 		}
 	}
 	__device__ __forceinline__ uint16_t le16(uint32_t o) const
 	{
 		const uint32_t r = o + m - wb;
-		if (r + 1 < WIN && (r & 3) != 3 && (FAST || o + 2 <= caplen))
+		if (r + 1 < wl && (r & 3) != 3 && (FAST || o + 2 <= caplen))
 			return (uint16_t)(dw(r >> 2) >> ((r & 3) * 8));
 		return (uint16_t)(b(o) | b(o + 1) << 8);
 	}
@@ -181,20 +187,20 @@ struct LSrc {
 	__device__ __forceinline__ bool in_window(uint32_t o, uint32_t nbytes) const
 	{
 		const uint32_t r = o + m - wb;
-		return r < WIN && r + nbytes <= WIN;
+		return r < wl && r + nbytes <= wl;
 	}
 	// window bytes from frame offset o to the window's end
 	__device__ __forceinline__ uint32_t window_bytes(uint32_t o) const
 	{
 		const uint32_t r = o + m - wb;
-		return r < WIN ? WIN - r : 0u;
+		return r < wl ? wl - r : 0u;
 	}
 	// the next layer would read past the staged window (the bytes its parse
 	// inspects from its start, c_step's `need`): general walk only
 	__device__ __forceinline__ bool near_end(uint32_t o, int id) const
 	{
 		const uint32_t need = step(id) >> 25;
-		return need && o < caplen && o + m + need > wb + WIN;
+		return need && o < caplen && o + m + need > wb + wl;
 	}
 	// sum of `nwords` little-endian u16 words from `o` (csum.h:16-17)
 	__device__ __forceinline__ uint32_t sum16(uint32_t o, uint32_t nwords) const
@@ -746,9 +752,40 @@ struct Walker {
 	uint64_t d;       // its packet's descriptor
 	uint32_t i;       // its packet's index
 	uint32_t wb;      // aligned position of its staged window
+	uint32_t wl;      // bytes of it staged
 	bool have;        // holds a packet
 	bool stage;       // its window must be (re)staged before it steps again
 };
+
+// How much of a walker's window to stage (walkers()).  An HBM read costs
+// whole 128-byte lines, and a chain's later layers need only a few bytes
+// each (c_step's `need`: 4 for an extension header, none for a leaf), so a
+// window that runs into the next line past the chain's end fetches a line
+// nothing reads.  The window ends at the end of the line holding the next
+// layer's needed bytes, or of the line after it when fewer than
+// NSD_WIN_AHEAD bytes of that line would be left past them (the chain then
+// likely goes on there); a walker whose next layer needs no bytes (a leaf)
+// stages nothing.  C4 (line model over the oracle's layer starts): 1.09
+// staged windows per packet against 0.93, 233 against 279 distinct bytes
+// per packet.
+#ifndef NSD_WIN_LINES
+#define NSD_WIN_LINES 1
+#endif
+#ifndef NSD_WIN_AHEAD
+#define NSD_WIN_AHEAD 32
+#endif
+__device__ __forceinline__ uint32_t window_len(uint64_t abs_wb, uint64_t abs_cur, uint32_t need)
+{
+	if (!NSD_WIN_LINES)
+		return WIN2;
+	if (!need)
+		return 0;
+	uint64_t le = ((abs_cur + need - 1) | 127) + 1;
+	if (le - (abs_cur + need) < NSD_WIN_AHEAD)
+		le += 128;
+	const uint64_t l = le - abs_wb;
+	return l < WIN2 ? (uint32_t)l : (uint32_t)WIN2;
+}
 
 // Hand the waiting packets (lanes with pnd: the tile's deferred packets, walk
 // state pw after walk_init / the fast walk's layers) to free walkers: the
@@ -775,17 +812,21 @@ __device__ __forceinline__ void walkers(Shared &sh, const uint8_t *__restrict__ 
 		const uint64_t off = NSD_DESC_OFF(wk.d);
 		const uint32_t caplen = NSD_DESC_CAPLEN(wk.d), m = (uint32_t)off & 15;
 		const bool st = wk.have && wk.stage;
-		if (st)
+		const uint64_t fbase = (uint64_t)(frames + (off & ~15ull));
+		if (st) {
 			wk.wb = (wk.w.data + m) & ~15u;
+			wk.wl = window_len(fbase + wk.wb, fbase + wk.w.data + m, sh.step[wk.w.id & 31] >> 25);
+		}
 		if (__ballot(st)) {
 			// (the window's HBM address and extent are recomputed from the
 			// descriptor rather than kept live across the walk: registers)
 			const uint32_t lim = caplen + m;   // first aligned position past the frame
-			stage_glds<WIN2>(&sh.win[wv][0], (uint64_t)(frames + (off & ~15ull)) + wk.wb,
-					 st && wk.wb < lim ? lim - wk.wb : 0u, lane);
+			uint32_t rem = st && wk.wb < lim ? lim - wk.wb : 0u;
+			rem = rem < wk.wl ? rem : wk.wl;
+			stage_glds<WIN2>(&sh.win[wv][0], fbase + wk.wb, rem, lane);
 		}
 		const LSrc<false, WIN2> src{ &sh.win[wv][lane * ROW], sh.lay3, sh.step, frames + off,
-					     caplen, m, wk.wb, false, swz_of((uint32_t)lane, WIN2 / 16) << 2 };
+					     caplen, m, wk.wb, false, swz_of((uint32_t)lane, WIN2 / 16) << 2, wk.wl };
 		bool susp;
 		for (;;) {
 			const bool run = wk.have && wk.w.id != 0;
@@ -866,7 +907,8 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 					   void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 					   uint32_t *__restrict__ ext_used, uint32_t chunk,
-					   const uint32_t *__restrict__ sll, Pending &pq)
+					   const uint32_t *__restrict__ sll, Pending &pq,
+					   unsigned long long *__restrict__ sched)
 {
 	constexpr int ROW = row_of(WIN1);
 	auto &s_win = sh.win;
@@ -917,6 +959,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	wk.d = 0;
 	wk.i = 0;
 	wk.wb = 0;
+	wk.wl = 0;
 	wk.have = false;
 	wk.stage = false;
 
@@ -949,7 +992,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			if (valid) {
 				const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
 							    (uint32_t)off & 15, 0, false };
-				fw = fast_walk<MODE>(src, caplen, w);
+				fw = fast_walk<MODE, false, NSD_FAST_EXT != 0>(src, caplen, w);
 			}
 			deferred = fw != FW_DONE;
 			ndefer += FlagCnt::pc(deferred);
@@ -1050,10 +1093,11 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 		d1 = d2;
 	}
 	fc.flush(s_cnt, lane);
-	if (lane == 0 && ndefer)
-		atomicAdd(&g_sched_acc[0], (unsigned long long)ndefer);
-	if (lane == 0 && pq.npend)
-		atomicAdd(&g_sched_acc[1], (unsigned long long)pq.npend);
+	// the schedule sample (a launch the launcher samples passes its pair)
+	if (sched && lane == 0 && ndefer)
+		atomicAdd(&sched[0], (unsigned long long)ndefer);
+	if (sched && lane == 0 && pq.npend)
+		atomicAdd(&sched[1], (unsigned long long)pq.npend);
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
@@ -1189,7 +1233,8 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 	void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
-	uint64_t *__restrict__ pend, uint32_t region, const uint32_t *__restrict__ sll)
+	uint64_t *__restrict__ pend, uint32_t region, const uint32_t *__restrict__ sll,
+	unsigned long long *__restrict__ sched)
 {
 	__shared__ Shared sh;
 	if (threadIdx.x < 64)
@@ -1203,7 +1248,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	// this wave's pending list (a wave visits region / WAVES packets)
 	Pending pq{ pend + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (region / WAVES), region / WAVES, 0,
 		    0 };
-	walk_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq);
+	walk_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq, sched);
 	if (MODE == PRINT_NORM || MODE == PRINT_LESS)
 		leaf_pass<MODE, CR>(frames, desc, rec, ext, pq);
 	if ((threadIdx.x & 63) == 0)
@@ -1664,7 +1709,8 @@ template <int MODE, bool CR>
 __global__ __launch_bounds__(BLOCK, CR ? NSD_FAST_MINW : NSD_FAST_MINW_FULL) void dissect_fast(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 	void *__restrict__ rec, unsigned long long *__restrict__ counters, uint4 *__restrict__ lists, uint32_t cap,
-	uint2 *__restrict__ cnts, const uint32_t *__restrict__ sll, uint32_t *__restrict__ side)
+	uint2 *__restrict__ cnts, const uint32_t *__restrict__ sll, uint32_t *__restrict__ side,
+	unsigned long long *__restrict__ sched)
 {
 	constexpr int SW = 2;
 	__shared__ FastShared sh;
@@ -1679,10 +1725,10 @@ __global__ __launch_bounds__(BLOCK, CR ? NSD_FAST_MINW : NSD_FAST_MINW_FULL) voi
 	if (lane == 0) {
 		cnts[gw] = make_uint2(ndef, nicmp);
 		sh.pcnt[wv] = nicmp;
-		if (ndef)
-			atomicAdd(&g_sched_acc[0], (unsigned long long)ndef);
-		if (nicmp)
-			atomicAdd(&g_sched_acc[1], (unsigned long long)nicmp);
+		if (sched && ndef)
+			atomicAdd(&sched[0], (unsigned long long)ndef);
+		if (sched && nicmp)
+			atomicAdd(&sched[1], (unsigned long long)nicmp);
 	}
 	if (MODE == PRINT_NORM) {
 		__syncthreads();   // records final, the block's pending lists and counts complete
@@ -1742,6 +1788,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
 	wk.d = 0;
 	wk.i = 0;
 	wk.wb = 0;
+	wk.wl = 0;
 	wk.have = false;
 	wk.stage = false;
 	WalkOut pw;
@@ -1866,15 +1913,17 @@ static size_t region_slots(uint32_t n)
 // the packets) the fused kernel wins too (0.70 - 0.75 against 0.73 - 0.81
 // ms on the same boxes, r03): its checksum pass streams at 4 waves per SIMD
 // with 8 loads in flight per lane.  Adaptive (the default): every
-// NSD_SCHED_SAMPLE launches on a device the launcher queues a copy of the
-// device's two sample counts (g_sched_acc: packets the fast walk handed
-// over, ICMPv4 messages left to a pass) to pinned host memory and resets
-// them; once a copy has landed, their shares of the packets pick the
+// NSD_SCHED_SAMPLE launches on a device, one launch is sampled: its kernels
+// count the packets the fast walk handed over and the ICMPv4 messages left
+// to a pass into a pair at the end of that launch's own workspace (zeroed
+// before it, copied to pinned host memory after it, on its stream), so
+// launches on other streams or pipes never mix into the sample.  Once the
+// copy has landed, the two shares of that launch's packets pick the
 // schedule for the launches after it, with hysteresis (fused above 15 %
 // deferred or 10 % pending checksums, split again below 5 % of both).  A
 // capture's traffic mix changes slowly against batches of a few
 // milliseconds; both schedules give identical results.  nsd_set_schedule
-// forces one (tests).
+// forces one (tests).  State is per device.
 #ifndef NSD_SCHED_SAMPLE
 #define NSD_SCHED_SAMPLE 32
 #endif
@@ -1882,16 +1931,15 @@ namespace {
 constexpr int MAX_DEV = 16;
 struct Sched {
 	bool init = false, fused = false, pending = false;
-	int launches = 0;
-	uint64_t pkts = 0, sampled = 0;   // packets since the last sample / in the sample in flight
-	unsigned long long *host = nullptr;
-	void *dev_acc = nullptr;
+	int launches = 0, last = 0;
+	uint64_t sampled = 0;                  // packets of the sampled launch in flight
+	unsigned long long *host = nullptr;    // its pair, copied back
 	hipEvent_t ev = nullptr;
+	int cus = 0;                           // compute units of the device
 };
 Sched g_sched[MAX_DEV];
 std::mutex g_sched_mu;
 int g_sched_force = 0;   // 0 adaptive, NSD_SCHED_SPLIT, NSD_SCHED_FUSED
-int g_sched_last = 0;
 
 int cur_dev()
 {
@@ -1901,14 +1949,27 @@ int cur_dev()
 	return d;
 }
 
-// the schedule of a launch of n packets on the current device
-bool sched_fused(uint32_t n)
+// The plan of one launch of n packets on the current device: the schedule,
+// and whether this launch is the sample (then its pair is zeroed on
+// `stream` here and copied back by sched_sampled after the kernels).
+struct Plan {
+	bool fused, sample;
+	int cus;
+};
+Plan sched_plan(uint32_t n, unsigned long long *pair, hipStream_t stream)
 {
 	std::lock_guard<std::mutex> g(g_sched_mu);
-	Sched &S = g_sched[cur_dev()];
-	bool fused;
+	const int dev = cur_dev();
+	Sched &S = g_sched[dev];
+	if (!S.cus) {
+		int cus = 0;
+		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+			cus = 256;
+		S.cus = cus;
+	}
+	Plan p{ false, false, S.cus };
 	if (g_sched_force) {
-		fused = g_sched_force == NSD_SCHED_FUSED;
+		p.fused = g_sched_force == NSD_SCHED_FUSED;
 	} else {
 		if (S.pending && hipEventQuery(S.ev) == hipSuccess) {
 			const double rd = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
@@ -1916,37 +1977,36 @@ bool sched_fused(uint32_t n)
 			S.fused = S.fused ? rd > 0.05 || ri > 0.05 : rd > 0.15 || ri > 0.10;
 			S.pending = false;
 		}
-		fused = S.fused;
+		p.fused = S.fused;
+		if (!S.init) {
+			S.init = true;
+			if (hipHostMalloc((void **)&S.host, 16, hipHostMallocDefault) != hipSuccess ||
+			    hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
+				S.host = nullptr;
+		}
+		if (++S.launches >= NSD_SCHED_SAMPLE && !S.pending && S.host && pair &&
+		    hipMemsetAsync(pair, 0, 16, stream) == hipSuccess) {
+			p.sample = true;
+			S.launches = 0;
+			S.sampled = n;
+			S.pending = true;   // (until its copy lands)
+		}
 	}
-	S.pkts += n;
-	S.launches++;
-	g_sched_last = fused ? NSD_SCHED_FUSED : NSD_SCHED_SPLIT;
-	return fused;
+	S.last = p.fused ? NSD_SCHED_FUSED : NSD_SCHED_SPLIT;
+	return p;
 }
 
-// after a launch on `stream`: queue the deferral sample when one is due
-void sched_sample(hipStream_t stream)
+// after the sampled launch's kernels on `stream`: bring its pair back
+void sched_sampled(unsigned long long *pair, hipStream_t stream)
 {
 	std::lock_guard<std::mutex> g(g_sched_mu);
 	Sched &S = g_sched[cur_dev()];
-	if (g_sched_force || S.pending || S.launches < NSD_SCHED_SAMPLE)
-		return;
-	if (!S.init) {
-		S.init = true;
-		if (hipHostMalloc((void **)&S.host, 16, hipHostMallocDefault) != hipSuccess ||
-		    hipGetSymbolAddress(&S.dev_acc, HIP_SYMBOL(nsd::g_sched_acc)) != hipSuccess ||
-		    hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
-			S.host = nullptr;
+	if (hipMemcpyAsync(S.host, pair, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+	    hipEventRecord(S.ev, stream) != hipSuccess) {
+		S.host[0] = S.host[1] = 0;
+		S.sampled = 0;
+		(void)hipEventRecord(S.ev, nullptr);
 	}
-	if (!S.host)
-		return;
-	if (hipMemcpyAsync(S.host, S.dev_acc, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-	    hipMemsetAsync(S.dev_acc, 0, 16, stream) != hipSuccess || hipEventRecord(S.ev, stream) != hipSuccess)
-		return;
-	S.sampled = S.pkts;
-	S.pkts = 0;
-	S.launches = 0;
-	S.pending = true;
 }
 } // namespace
 
@@ -1963,17 +2023,22 @@ extern "C" int nsd_set_schedule(int sched)
 extern "C" int nsd_last_schedule(void)
 {
 	std::lock_guard<std::mutex> g(g_sched_mu);
-	return g_sched_last;
+	return g_sched[cur_dev()].last;
 }
 
 // workspace: the fused kernel's pending lists (u64 per slot); the split
 // schedule's fast lists (up to 32 bytes per slot), their counts and the
 // walker kernel's pending lists (u64 per slot, up to two per packet slot)
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
+// (the last 256 bytes: the schedule sample's pair, at sched_pair_at)
+static size_t sched_pair_at(uint32_t n)
 {
 	const size_t slots = region_slots(n);
-	return align256(32 * slots) + align256((size_t)NSD_MAX_GRID * nsd::WAVES * 8) + 16 * slots + 256;
+	return align256(align256(32 * slots) + align256((size_t)NSD_MAX_GRID * nsd::WAVES * 8) + 16 * slots);
+}
+extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
+{
+	return sched_pair_at(n) + 256;
 }
 
 extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d_desc, const void *d_sll,
@@ -2010,13 +2075,6 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	using namespace nsd;
 	if (n == 0)
 		return 0;
-	static int s_cus = 0;
-	if (!s_cus) {
-		int dev = 0;
-		if (hipGetDevice(&dev) != hipSuccess ||
-		    hipDeviceGetAttribute(&s_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-			s_cus = 256;
-	}
 	const int mi = mode == PRINT_NORM ? 0 : mode == PRINT_LESS ? 1 : 2;
 	const int ci = compact ? 1 : 0;
 	const uint32_t waves = (n + 63) / 64;
@@ -2034,25 +2092,32 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	};
 	// persistent grids: exactly the blocks that are resident together (CUs x
 	// the kernel's occupancy), so no block waits for a second round; every
-	// block grid-strides (counters then cost one flush per block)
-	auto occupancy = [&](const void *f, int &slot, int dflt) {
-		if (!slot) {
-			int occ = 0;
+	// block grid-strides (counters then cost one flush per block).  The
+	// occupancy of a kernel is a property of its code (one gfx950 build):
+	// cached once, racing callers store the same value.
+	auto occupancy = [&](const void *f, std::atomic<int> &slot, int dflt) {
+		int occ = slot.load(std::memory_order_relaxed);
+		if (!occ) {
 			if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, BLOCK, 0) != hipSuccess || occ < 1)
 				occ = dflt;
-			slot = occ;
+			slot.store(occ, std::memory_order_relaxed);
 		}
-		return slot;
+		return occ;
 	};
-	const bool fused = mi != 2 && sched_fused(n);
+	unsigned long long *const pair = d_ws ? (unsigned long long *)((uint8_t *)d_ws + sched_pair_at(n)) : nullptr;
+	const Plan plan = sched_plan(n, mi != 2 ? pair : nullptr, stream);
+	const int s_cus = plan.cus;
+	unsigned long long *const sched = plan.sample ? pair : nullptr;
+	const bool fused = mi != 2 && plan.fused;
 	if (fused) {
 	typedef void (*kfn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, uint32_t *, uint32_t,
-			    uint32_t *, uint32_t, unsigned long long *, uint64_t *, uint32_t, const uint32_t *);
+			    uint32_t *, uint32_t, unsigned long long *, uint64_t *, uint32_t, const uint32_t *,
+			    unsigned long long *);
 	static const kfn kernels[2][3] = {
 		{ dissect_all<PRINT_NORM, false>, dissect_all<PRINT_LESS, false>, dissect_all<PRINT_HEX, false> },
 		{ dissect_all<PRINT_NORM, true>, dissect_all<PRINT_LESS, true>, dissect_all<PRINT_HEX, true> },
 	};
-	static int s_occ[2][3];
+	static std::atomic<int> s_occ[2][3];
 	const kfn f = kernels[ci][mi];
 	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)(s_cus * occupancy((const void *)f, s_occ[ci][mi], 4));
 	if (cap_blocks > NSD_MAX_GRID)
@@ -2060,14 +2125,15 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	const uint32_t blocks = want < cap_blocks ? want : cap_blocks;
 	hipLaunchKernelGGL(f, dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec, d_ext,
 			   ext_words, d_ext_used, chunk_for(blocks), (unsigned long long *)d_counters, (uint64_t *)d_ws,
-			   region_for(n, blocks), (const uint32_t *)d_sll);
+			   region_for(n, blocks), (const uint32_t *)d_sll, sched);
 	if (hipGetLastError() != hipSuccess)
 		return -2;
-	sched_sample(stream);
+	if (sched)
+		sched_sampled(sched, stream);
 	return 0;
 	}
 	typedef void (*ffn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, unsigned long long *, uint4 *,
-			    uint32_t, uint2 *, const uint32_t *, uint32_t *);
+			    uint32_t, uint2 *, const uint32_t *, uint32_t *, unsigned long long *);
 	typedef void (*wfn)(const uint8_t *, const uint64_t *, uint32_t, void *, uint32_t *, uint32_t, uint32_t *,
 			    uint32_t, unsigned long long *, const uint4 *, uint32_t, const uint2 *, uint32_t, uint64_t *,
 			    uint32_t);
@@ -2079,7 +2145,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 		{ dissect_walk<PRINT_NORM, false>, dissect_walk<PRINT_LESS, false> },
 		{ dissect_walk<PRINT_NORM, true>, dissect_walk<PRINT_LESS, true> },
 	};
-	static int s_focc[2][3], s_wocc[2][2];
+	static std::atomic<int> s_focc[2][3], s_wocc[2][2];
 	// grid > 0 (tests): both kernels' grids capped at `grid` blocks
 	uint32_t fcap = grid > 0 ? (uint32_t)grid
 				 : (uint32_t)(s_cus * occupancy((const void *)fast[ci][mi], s_focc[ci][mi], 8));
@@ -2100,7 +2166,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	// compact records: the pool's side words (when it has them), for leaf ends
 	uint32_t *side = compact && d_ext && ext_words >= n ? d_ext : nullptr;
 	hipLaunchKernelGGL(fast[ci][mi], dim3(fblocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec,
-			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll, side);
+			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll, side, sched);
 	if (hipGetLastError() != hipSuccess)
 		return -2;
 	if (mi == 2)
@@ -2118,7 +2184,8 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 			   nlists, pend, per_wave * cap * WAVES);
 	if (hipGetLastError() != hipSuccess)
 		return -2;
-	sched_sample(stream);
+	if (sched)
+		sched_sampled(sched, stream);
 	return 0;
 }
 
