@@ -27,6 +27,7 @@
 // block at the end.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <atomic>
 #include <mutex>
@@ -1291,6 +1292,9 @@ constexpr int FROW = WIN1 / 4;   // fast rows: 16 dwords, 16-byte slots XOR-swiz
 #ifndef NSD_FAST_MINW_FULL
 #define NSD_FAST_MINW_FULL (NSD_FAST_DEPTH > 1 ? 4 : 5)   // the same for 16-byte records (the deferral entries carry layer starts)
 #endif
+#ifndef NSD_PLAIN_COUNT
+#define NSD_PLAIN_COUNT 1          // plain tiles count from three ballots (dissect_fast)
+#endif
 #ifndef NSD_FAST_BPC
 #define NSD_FAST_BPC (NSD_FAST_DEPTH > 1 ? 3 : 0)   // resident fast blocks per CU (0: as many as fit)
 #endif
@@ -1473,6 +1477,29 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 		const bool deferred = fw != FW_DONE;
 		wave_sync_lds();
 		const bool done = valid && !deferred;
+		if (NSD_PLAIN_COUNT && plain) {
+			// a plain tile (Ethernet / IPv4 / TCP or UDP, every packet done, no
+			// ICMPv4, no leaf, no deferral): its counts straight from three
+			// ballots - packets, bad IPv4 sums, trims - and the TCP share
+			const uint64_t vm = __ballot(valid), tm = __ballot(valid && w.chain >> 10 == NSD_OPS_TCP);
+			const uint32_t nv = (uint32_t)__popcll(vm), nt = (uint32_t)__popcll(tm);
+			if (lane == 0) {
+				atomicAdd(&sh.ops[NSD_OPS_ETHERNET], nv);
+				atomicAdd(&sh.ops[NSD_OPS_IPV4], nv);
+				if (nt)
+					atomicAdd(&sh.ops[NSD_OPS_TCP], nt);
+				if (nv - nt)
+					atomicAdd(&sh.ops[NSD_OPS_UDP], nv - nt);
+			}
+			if (valid)
+				put_rec_st<CR>(rec, i, w);
+			fc.pkts += nv;
+			fc.ipbad += FlagCnt::pc(valid && w.ip_csum != 0);
+			fc.trim += FlagCnt::pc(valid && w.tail < caplen);
+			if (valid)
+				fc.bytes += caplen;
+			return;
+		}
 		if (MODE == PRINT_NORM) {
 			// ICMPv4 messages past the window, from the back of the list
 			const bool pnd = w.icmp_pend && done;
@@ -1923,17 +1950,29 @@ static size_t region_slots(uint32_t n)
 // deferred or 10 % pending checksums, split again below 5 % of both).  A
 // capture's traffic mix changes slowly against batches of a few
 // milliseconds; both schedules give identical results.  nsd_set_schedule
-// forces one (tests).  State is per device.
+// forces one (tests).  The same sample brings back the launch's packet and
+// byte counts (the counter vector before and after it): when its frames
+// average at most NSD_SMALL_FRAME bytes, the fast kernel runs
+// NSD_FAST_BPC_SMALL blocks per CU instead of NSD_FAST_BPC (C2's 64-byte
+// frames stream from few waves: 0.217 -> 0.207 ms at 2 blocks per CU on one
+// box, where IMIX frames need the third: 0.78 against 0.92 ms).  State is
+// per device.
 #ifndef NSD_SCHED_SAMPLE
 #define NSD_SCHED_SAMPLE 32
 #endif
 namespace {
 constexpr int MAX_DEV = 16;
+#ifndef NSD_SMALL_FRAME
+#define NSD_SMALL_FRAME 128
+#endif
+#ifndef NSD_FAST_BPC_SMALL
+#define NSD_FAST_BPC_SMALL 2
+#endif
 struct Sched {
-	bool init = false, fused = false, pending = false;
+	bool init = false, fused = false, pending = false, small = false;
 	int launches = 0, last = 0;
 	uint64_t sampled = 0;                  // packets of the sampled launch in flight
-	unsigned long long *host = nullptr;    // its pair, copied back
+	unsigned long long *host = nullptr;    // its pair, then its counters [32, 34) before and after
 	hipEvent_t ev = nullptr;
 	int cus = 0;                           // compute units of the device
 };
@@ -1953,10 +1992,10 @@ int cur_dev()
 // and whether this launch is the sample (then its pair is zeroed on
 // `stream` here and copied back by sched_sampled after the kernels).
 struct Plan {
-	bool fused, sample;
+	bool fused, sample, small;
 	int cus;
 };
-Plan sched_plan(uint32_t n, unsigned long long *pair, hipStream_t stream)
+Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, hipStream_t stream)
 {
 	std::lock_guard<std::mutex> g(g_sched_mu);
 	const int dev = cur_dev();
@@ -1967,43 +2006,46 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, hipStream_t stream)
 			cus = 256;
 		S.cus = cus;
 	}
-	Plan p{ false, false, S.cus };
-	if (g_sched_force) {
-		p.fused = g_sched_force == NSD_SCHED_FUSED;
-	} else {
-		if (S.pending && hipEventQuery(S.ev) == hipSuccess) {
-			const double rd = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
-			const double ri = S.sampled ? (double)S.host[1] / (double)S.sampled : 0.0;
-			S.fused = S.fused ? rd > 0.05 || ri > 0.05 : rd > 0.15 || ri > 0.10;
-			S.pending = false;
-		}
-		p.fused = S.fused;
-		if (!S.init) {
-			S.init = true;
-			if (hipHostMalloc((void **)&S.host, 16, hipHostMallocDefault) != hipSuccess ||
-			    hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
-				S.host = nullptr;
-		}
-		if (++S.launches >= NSD_SCHED_SAMPLE && !S.pending && S.host && pair &&
-		    hipMemsetAsync(pair, 0, 16, stream) == hipSuccess) {
-			p.sample = true;
-			S.launches = 0;
-			S.sampled = n;
-			S.pending = true;   // (until its copy lands)
-		}
+	Plan p{ false, false, false, S.cus };
+	if (S.pending && hipEventQuery(S.ev) == hipSuccess) {
+		const double rd = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
+		const double ri = S.sampled ? (double)S.host[1] / (double)S.sampled : 0.0;
+		S.fused = S.fused ? rd > 0.05 || ri > 0.05 : rd > 0.15 || ri > 0.10;
+		const uint64_t pk = S.host[4] - S.host[2], by = S.host[5] - S.host[3];
+		if (pk)
+			S.small = by <= (uint64_t)NSD_SMALL_FRAME * pk;
+		S.pending = false;
+	}
+	if (!S.init) {
+		S.init = true;
+		if (hipHostMalloc((void **)&S.host, 64, hipHostMallocDefault) != hipSuccess ||
+		    hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
+			S.host = nullptr;
+	}
+	p.fused = g_sched_force ? g_sched_force == NSD_SCHED_FUSED : S.fused;
+	p.small = S.small;
+	if (++S.launches >= NSD_SCHED_SAMPLE && !S.pending && S.host && pair && counters &&
+	    hipMemsetAsync(pair, 0, 16, stream) == hipSuccess &&
+	    hipMemcpyAsync(S.host + 2, counters + NSD_CNT_PKTS, 16, hipMemcpyDeviceToHost, stream) == hipSuccess) {
+		p.sample = true;
+		S.launches = 0;
+		S.sampled = n;
+		S.pending = true;   // (until its copy lands)
 	}
 	S.last = p.fused ? NSD_SCHED_FUSED : NSD_SCHED_SPLIT;
 	return p;
 }
 
-// after the sampled launch's kernels on `stream`: bring its pair back
-void sched_sampled(unsigned long long *pair, hipStream_t stream)
+// after the sampled launch's kernels on `stream`: bring its pair and
+// counters back
+void sched_sampled(unsigned long long *pair, const uint64_t *counters, hipStream_t stream)
 {
 	std::lock_guard<std::mutex> g(g_sched_mu);
 	Sched &S = g_sched[cur_dev()];
 	if (hipMemcpyAsync(S.host, pair, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+	    hipMemcpyAsync(S.host + 4, counters + NSD_CNT_PKTS, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
 	    hipEventRecord(S.ev, stream) != hipSuccess) {
-		S.host[0] = S.host[1] = 0;
+		memset(S.host, 0, 48);
 		S.sampled = 0;
 		(void)hipEventRecord(S.ev, nullptr);
 	}
@@ -2105,7 +2147,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 		return occ;
 	};
 	unsigned long long *const pair = d_ws ? (unsigned long long *)((uint8_t *)d_ws + sched_pair_at(n)) : nullptr;
-	const Plan plan = sched_plan(n, mi != 2 ? pair : nullptr, stream);
+	const Plan plan = sched_plan(n, mi != 2 ? pair : nullptr, d_counters, stream);
 	const int s_cus = plan.cus;
 	unsigned long long *const sched = plan.sample ? pair : nullptr;
 	const bool fused = mi != 2 && plan.fused;
@@ -2129,7 +2171,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	if (hipGetLastError() != hipSuccess)
 		return -2;
 	if (sched)
-		sched_sampled(sched, stream);
+		sched_sampled(sched, d_counters, stream);
 	return 0;
 	}
 	typedef void (*ffn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, unsigned long long *, uint4 *,
@@ -2150,9 +2192,11 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	uint32_t fcap = grid > 0 ? (uint32_t)grid
 				 : (uint32_t)(s_cus * occupancy((const void *)fast[ci][mi], s_focc[ci][mi], 8));
 	// with two tiles in flight per wave, 3 blocks per CU outrun the 4 that
-	// fit (HBM serves fewer concurrent streams better)
-	if (grid <= 0 && NSD_FAST_BPC > 0 && fcap > (uint32_t)(s_cus * NSD_FAST_BPC))
-		fcap = (uint32_t)(s_cus * NSD_FAST_BPC);
+	// fit (HBM serves fewer concurrent streams better), and 2
+	// the 3 when the frames are small (the sample, sched_plan)
+	const int bpc = plan.small ? NSD_FAST_BPC_SMALL : NSD_FAST_BPC;
+	if (grid <= 0 && bpc > 0 && fcap > (uint32_t)(s_cus * bpc))
+		fcap = (uint32_t)(s_cus * bpc);
 	if (fcap > NSD_MAX_GRID)
 		fcap = NSD_MAX_GRID;
 	const uint32_t fblocks = want < fcap ? want : fcap;
@@ -2185,7 +2229,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	if (hipGetLastError() != hipSuccess)
 		return -2;
 	if (sched)
-		sched_sampled(sched, stream);
+		sched_sampled(sched, d_counters, stream);
 	return 0;
 }
 

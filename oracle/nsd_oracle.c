@@ -2077,7 +2077,22 @@ void nsor_frame_hdr(const nsd_frame_hdr_t *fh, const nsd_sll_t *sll, const uint8
 		memcpy(&pid, pkt + 12, 4);                   /* nlmsghdr.nlmsg_pid */
 		pkttype = pid == 0 ? 7 : 6;                  /* PACKET_KERNEL : PACKET_USER */
 	}
-	ifn = if_indextoname((unsigned)sll->ifindex, tmp);
+	/* if_indextoname (dissector.h:82, 89), the last answer kept per thread:
+	 * the reference asks the kernel for every packet (a socket and an
+	 * ioctl), which would make the timed CPU baseline a syscall benchmark;
+	 * the name of an index does not change while a capture runs */
+	{
+		static __thread int last_idx = -1, last_ok;
+		static __thread char last_name[64];
+		if (sll->ifindex != last_idx) {
+			const char *r = if_indextoname((unsigned)sll->ifindex, tmp);
+			last_idx = sll->ifindex;
+			last_ok = r != NULL;
+			if (r)
+				snprintf(last_name, sizeof(last_name), "%s", r);
+		}
+		ifn = last_ok ? last_name : NULL;
+	}
 	switch (mode) {
 	case PRINT_LESS:
 		T(t, "%s %s %u #%lu", fh_packet_types[pkttype] ? fh_packet_types[pkttype] : "?", ifn ? ifn : "?",
