@@ -1357,6 +1357,12 @@ __device__ __forceinline__ uint32_t fold_weighted(uint32_t sum, bool odd)
 // fast_walk's result from them alone (re-read rather than kept: registers).
 // A tile takes this path only when every valid lane's packet is plain
 // (wave-uniform), so a mixed tile runs fast_walk alone.
+// plain_is / plain_walk map protocol 6 / 17 to TCP / UDP without the eth_lay3
+// lookup fast_walk makes: the table must agree
+constexpr uint8_t k_plain_lay3[256] = NSD_LAY3_TABLE;
+static_assert(k_plain_lay3[6] == NSD_OPS_TCP && k_plain_lay3[17] == NSD_OPS_UDP,
+	      "plain_walk's protocol map differs from eth_lay3");
+
 __device__ __forceinline__ bool plain_is(const LSrc<true, WIN1> &s, uint32_t caplen)
 {
 	const uint32_t r = s.m + 12, j = r >> 2, sh = r & 3;

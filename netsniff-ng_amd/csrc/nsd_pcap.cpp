@@ -25,14 +25,21 @@
 //     path (nsd_proto.cpp), in file order.
 #include <errno.h>
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <sys/uio.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -76,14 +83,20 @@ struct nsd_pcap {
 	uint32_t magic = 0;      // in host order
 	bool nsec = false;
 	bool eof = false;
-	// buffered reader (the scatter-gather reader's iovecs, pcap_sg.c)
+	// buffered reader (the scatter-gather reader's iovecs, pcap_sg.c), or a
+	// regular file mapped whole (pcap_mm.c's way; the replay's reader then
+	// only scans the record headers and the pool copies the bodies)
 	std::vector<uint8_t> buf;
+	const uint8_t *map = nullptr;
 	size_t pos = 0, len = 0;
 
+	const uint8_t *data() const { return map ? map : buf.data(); }
 	bool fill(size_t need)
 	{
 		if (len - pos >= need)
 			return true;
+		if (map)
+			return false;
 		if (pos) {
 			memmove(buf.data(), buf.data() + pos, len - pos);
 			len -= pos;
@@ -112,13 +125,24 @@ extern "C" nsd_pcap *nsd_pcap_open(const char *path)
 		return nullptr;
 	nsd_pcap *p = new nsd_pcap;
 	p->fd = fd;
-	p->buf.resize(4 << 20);
+	struct stat sb;
+	const char *mm = getenv("NSD_PCAP_MMAP");
+	if (!(mm && mm[0] == '0') && fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode) && sb.st_size >= 24) {
+		void *m = mmap(nullptr, (size_t)sb.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+		if (m != MAP_FAILED) {
+			(void)madvise(m, (size_t)sb.st_size, MADV_SEQUENTIAL);
+			p->map = (const uint8_t *)m;
+			p->len = (size_t)sb.st_size;
+		}
+	}
+	if (!p->map)
+		p->buf.resize(4 << 20);
 	uint8_t h[24];
 	if (!p->fill(24)) {
 		nsd_pcap_close(p);
 		return nullptr;
 	}
-	memcpy(h, p->buf.data(), 24);
+	memcpy(h, p->data(), 24);
 	p->pos = 24;
 	uint32_t magic, lt;
 	memcpy(&magic, h, 4);
@@ -161,6 +185,8 @@ extern "C" void nsd_pcap_close(nsd_pcap *p)
 {
 	if (!p)
 		return;
+	if (p->map)
+		munmap((void *)p->map, p->len);
 	if (p->fd >= 0)
 		close(p->fd);
 	delete p;
@@ -263,7 +289,7 @@ static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *des
 			p->eof = true;
 			break;
 		}
-		const uint8_t *h = p->buf.data() + p->pos;
+		const uint8_t *h = p->data() + p->pos;
 		uint32_t sec, frac, cl, wl;
 		memcpy(&sec, h, 4);
 		memcpy(&frac, h + 4, 4);
@@ -295,7 +321,7 @@ static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *des
 			p->eof = true;
 			break;
 		}
-		h = p->buf.data() + p->pos;
+		h = p->data() + p->pos;
 		memcpy(frames + at, h + p->hdrsize, caplen);
 		p->pos += p->hdrsize + caplen;
 		desc[n] = NSD_DESC(at, caplen);
@@ -314,6 +340,68 @@ static long read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *des
 	return n;
 }
 
+// A mapped file's next batch, as read_batch lays it out (same checks, same
+// stops), without touching the bodies: desc[k] = the record's place in the
+// batch buffer, src[k] = its header's offset in the file.  fill_range copies
+// a range of the batch afterwards (the replay runs those on its pool).
+// *end = the bytes the batch uses.
+static long scan_batch(nsd_pcap *p, size_t cap, nsd_desc_t *desc, uint64_t *src, uint32_t max_n, size_t *end)
+{
+	size_t off = 0;
+	uint32_t n = 0;
+	const uint32_t hs = p->hdrsize;
+	while (n < max_n && !p->eof) {
+		if (p->len - p->pos < hs) {
+			p->eof = true;
+			break;
+		}
+		uint32_t cl;
+		memcpy(&cl, p->map + p->pos + 8, 4);
+		if (p->swapped)
+			cl = bswap32(cl);
+		const uint32_t caplen = cl - p->ll_extra;
+		if (caplen == 0 || caplen > REPLAY_BUF) {
+			p->eof = true;
+			break;
+		}
+		if (caplen > NSD_MAX_CAPLEN) {
+			if (n == 0)
+				return NSD_ERR_CAPLEN;
+			break;
+		}
+		const size_t at = (off + 15) & ~(size_t)15;
+		if (at + caplen + NSD_FRAME_PAD > cap) {
+			if (n == 0)
+				return NSD_ERR_ARG;
+			break;
+		}
+		if (p->len - p->pos < (size_t)hs + caplen) {
+			p->eof = true;
+			break;
+		}
+		src[n] = p->pos;
+		desc[n] = NSD_DESC(at, caplen);
+		p->pos += hs + caplen;
+		off = at + caplen;
+		n++;
+	}
+	*end = off;
+	return n;
+}
+
+static void fill_range(const nsd_pcap *p, uint8_t *frames, const nsd_desc_t *desc, const uint64_t *src,
+		       uint32_t lo, uint32_t hi, nsd_sll_t *sll, nsd_frame_hdr_t *fh, uint8_t *rhdr)
+{
+	const uint32_t hs = p->hdrsize;
+	for (uint32_t k = lo; k < hi; k++) {
+		const uint8_t *h = p->map + src[k];
+		memcpy(frames + NSD_DESC_OFF(desc[k]), h + hs, NSD_DESC_CAPLEN(desc[k]));
+		if (rhdr)
+			memcpy(rhdr + 32 * (size_t)k, h, hs);
+		record_meta(p, h, sll + k, fh + k);
+	}
+}
+
 // The next record whatever its length (<= the 1 MiB replay buffer), for the
 // records a batch cannot carry: its bytes into `frame`, its header as stored
 // into rhdr (may be NULL), its sockaddr_ll / frame header fields into *sll /
@@ -325,7 +413,7 @@ static long read_one(nsd_pcap *p, std::vector<uint8_t> &frame, nsd_sll_t *sll, n
 		p->eof = true;
 		return 0;
 	}
-	const uint8_t *h = p->buf.data() + p->pos;
+	const uint8_t *h = p->data() + p->pos;
 	uint32_t cl;
 	memcpy(&cl, h + 8, 4);
 	if (p->swapped)
@@ -335,7 +423,7 @@ static long read_one(nsd_pcap *p, std::vector<uint8_t> &frame, nsd_sll_t *sll, n
 		p->eof = true;
 		return 0;
 	}
-	h = p->buf.data() + p->pos;
+	h = p->data() + p->pos;
 	frame.assign(h + p->hdrsize, h + p->hdrsize + caplen);
 	frame.resize((size_t)caplen + NSD_FRAME_PAD, 0);
 	if (rhdr)
@@ -410,6 +498,13 @@ constexpr int NSLOT = DEPTH + 3;   // + being rendered, rendered, being written
 // layer) entry; a chain the pool cannot hold is rendered per packet
 constexpr uint32_t EXT_WORDS = BATCH + BATCH / 4 * NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS);
 
+// one formatter part's text: a cache line of its own, as every append writes
+// the string's length (adjacent std::strings shared lines between the pool's
+// threads: per-packet false sharing that cost the 16-thread pool 3x per record)
+struct alignas(64) TextPart {
+	std::string s;
+};
+
 struct ReplayRes {
 	nsd_pipe *pipe = nullptr;
 	struct {
@@ -421,10 +516,12 @@ struct ReplayRes {
 	} buf[NSLOT] = {};
 	// each record's frame header fields (show_frame_hdr)
 	std::vector<nsd_frame_hdr_t> fh[NSLOT];
+	// a mapped file's record offsets (scan_batch)
+	std::vector<uint64_t> src[NSLOT];
 	// the formatter parts' text buffers per slot, kept with their capacity:
 	// regrown per replay they faulted in hundreds of MB of fresh pages,
 	// with the formatter threads queued on the page-table lock
-	std::vector<std::string> part[NSLOT];
+	std::vector<TextPart> part[NSLOT];
 	bool ready() const { return pipe != nullptr; }
 	long create(int lt, int mode)
 	{
@@ -444,6 +541,8 @@ struct ReplayRes {
 		}
 		for (auto &v : fh)
 			v.resize(BATCH);
+		for (auto &v : src)
+			v.resize(BATCH);
 		return NSD_OK;
 	}
 	void release()
@@ -457,15 +556,97 @@ struct ReplayRes {
 			x = {};
 		}
 		for (auto &v : part)
-			std::vector<std::string>().swap(v);
+			std::vector<TextPart>().swap(v);
 		for (auto &v : fh)
 			std::vector<nsd_frame_hdr_t>().swap(v);
+		for (auto &v : src)
+			std::vector<uint64_t>().swap(v);
 		nsd_pipe_destroy(pipe);
 		pipe = nullptr;
 	}
 };
 std::mutex g_replay_mu;
 ReplayRes g_replay;
+
+// The CPUs the formatter pool runs on: one per physical core (an SMT
+// sibling formats at a fraction of a core's rate), those of the calling
+// thread's NUMA node first, of the CPUs this process may use.  Empty when
+// the topology cannot be read (then nothing is pinned), or NSD_REPLAY_PIN=0.
+std::vector<int> pool_cpus()
+{
+	std::vector<int> out;
+	const char *e = getenv("NSD_REPLAY_PIN");
+	if (e && e[0] == '0')
+		return out;
+	cpu_set_t set;
+	if (sched_getaffinity(0, sizeof(set), &set) != 0)
+		return out;
+	auto rd = [](int cpu, const char *what) -> long {
+		char path[128];
+		snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/%s", cpu, what);
+		FILE *f = fopen(path, "r");
+		if (!f)
+			return -1;
+		long v = -1;
+		if (fscanf(f, "%ld", &v) != 1)
+			v = -1;
+		fclose(f);
+		return v;
+	};
+	auto node_of = [](int cpu) -> int {
+		for (int n = 0; n < 64; n++) {
+			char path[128];
+			snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/node%d", cpu, n);
+			if (access(path, F_OK) == 0)
+				return n;
+		}
+		return 0;
+	};
+	const int me = sched_getcpu();
+	const int my_node = me >= 0 ? node_of(me) : 0;
+	std::vector<std::pair<long, long>> seen;   // (package, core)
+	std::vector<int> near, far;
+	for (int c = 0; c < CPU_SETSIZE; c++) {
+		if (!CPU_ISSET(c, &set))
+			continue;
+		const long pkg = rd(c, "topology/physical_package_id"), core = rd(c, "topology/core_id");
+		if (pkg < 0 || core < 0)
+			return {};
+		bool dup = false;
+		for (auto &x : seen)
+			dup = dup || (x.first == pkg && x.second == core);
+		if (dup)
+			continue;
+		seen.emplace_back(pkg, core);
+		(node_of(c) == my_node ? near : far).push_back(c);
+	}
+	out = near;
+	out.insert(out.end(), far.begin(), far.end());
+	// the caller's core first (the pool leaves it to the reader)
+	if (me >= 0) {
+		const long mp = rd(me, "topology/physical_package_id"), mc = rd(me, "topology/core_id");
+		for (size_t k = 0; k < out.size(); k++)
+			if (rd(out[k], "topology/physical_package_id") == mp && rd(out[k], "topology/core_id") == mc) {
+				std::swap(out[0], out[k]);
+				break;
+			}
+	}
+	return out;
+}
+
+// Stage times of one replay, printed to stderr when NSD_REPLAY_STATS is set
+// in the environment (the pipeline's balance on a given host): the reader,
+// the device waits, the formatter jobs (summed over the pool), the writer,
+// and the reader's waits for a free slot.
+struct ReplayStats {
+	std::atomic<uint64_t> read{ 0 }, dev{ 0 }, fmt{ 0 }, write{ 0 }, slot{ 0 }, jobs{ 0 };
+	static uint64_t now()
+	{
+		return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+			       std::chrono::steady_clock::now().time_since_epoch())
+			.count();
+	}
+};
 } // namespace
 
 // As nsd_replay_pcap; with pcap_fd >= 0 also the `--out f.pcap` write-out
@@ -515,6 +696,11 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	ReplayRes own;
 	ReplayRes &res = cache_lk.owns_lock() ? g_replay : own;
 	long rc = res.ready() ? (long)nsd_pipe_retarget(res.pipe, lt, mode) : (long)res.create(lt, mode);
+	if (rc == 1) {
+		// the cached set was made on another device than the current one
+		res.release();
+		rc = res.create(lt, mode);
+	}
 	if (rc != NSD_OK) {
 		nsd_pcap_close(p);
 		return rc;
@@ -526,6 +712,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		nsd_sll_t *sll = nullptr;
 		uint8_t *rhdr = nullptr;   // record headers as read (pcap write-out)
 		nsd_frame_hdr_t *fh = nullptr;
+		uint64_t *src = nullptr;   // record offsets in a mapped file
+		int fill_left = 0;         // copy jobs of the batch not done
 		uint64_t count0 = 0;       // the packet counter of the batch's first record
 		nsd_crec *rec = nullptr;
 		uint32_t *ext = nullptr;
@@ -535,7 +723,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		int status = 0;
 		uint64_t seq = 0;
 		int parts = 0, left = 0;   // render jobs, jobs not done
-		std::vector<std::string> *part = nullptr;   // res.part[slot]
+		std::vector<TextPart> *part = nullptr;   // res.part[slot]
 		long prc = NSD_OK;         // first render error
 	};
 	std::vector<Slot> b(NSLOT);
@@ -549,6 +737,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		x.ext = res.buf[k].ext;
 		x.sll = res.buf[k].sll;
 		x.fh = res.fh[k].data();
+		x.src = res.src[k].data();
 		x.verdict = filter ? &verdicts[(size_t)k * BATCH] : nullptr;
 		x.rhdr = pcap_fd >= 0 ? &rhdrs[(size_t)k * BATCH * 32] : nullptr;
 		x.part = &res.part[k];
@@ -557,8 +746,16 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	}
 
 	std::mutex mu;
-	std::condition_variable cv_job, cv_write, cv_free;
-	std::deque<std::pair<int, int>> jobs;   // (slot, part)
+	std::condition_variable cv_job, cv_write, cv_free, cv_fill;
+	ReplayStats st;
+	const bool stats = getenv("NSD_REPLAY_STATS") != nullptr;
+	const uint64_t t_start = ReplayStats::now();
+	// (slot, part, parts): render jobs, and copy jobs (parts > 0) of a mapped
+	// file's batch, which go first
+	struct Job {
+		int slot, part, parts;
+	};
+	std::deque<Job> jobs;
 	std::vector<int> free_slots;
 	for (int k = NSLOT - 1; k >= 0; k--)
 		free_slots.push_back(k);
@@ -585,7 +782,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	auto put_parts = [&](const Slot &x) -> long {
 		if (cols > 0) {
 			for (int t = 0; t < x.parts; t++) {
-				const long r = put_text((*x.part)[t]);
+				const long r = put_text((*x.part)[t].s);
 				if (r != NSD_OK)
 					return r;
 			}
@@ -593,8 +790,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		}
 		std::vector<struct iovec> iov;
 		for (int t = 0; t < x.parts; t++)
-			if (!(*x.part)[t].empty())
-				iov.push_back({ (void *)(*x.part)[t].data(), (*x.part)[t].size() });
+			if (!(*x.part)[t].s.empty())
+				iov.push_back({ (void *)(*x.part)[t].s.data(), (*x.part)[t].s.size() });
 		size_t k = 0;
 		while (k < iov.size()) {
 			const int cnt = (int)(iov.size() - k < 512 ? iov.size() - k : 512);
@@ -630,46 +827,107 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	// formatter pool: part t of a slot = its packets [n t / parts, n (t+1) / parts)
 	auto render = [&](Slot &x, int t) -> long {
 		const uint32_t lo = (uint32_t)((uint64_t)x.n * t / x.parts), hi = (uint32_t)((uint64_t)x.n * (t + 1) / x.parts);
-		std::string &s = (*x.part)[t];
+		// (locals: appends through a char * would reload every captured field)
+		const uint8_t *const frames = x.frames;
+		const nsd_desc_t *const desc = x.desc;
+		const nsd_frame_hdr_t *const fh = x.fh;
+		const nsd_sll_t *const sll = x.sll;
+		const nsd_crec *const rec = x.rec;
+		const uint32_t *const ext = x.ext;
+		const uint64_t count0 = x.count0;
+		const int lt_ = lt, mode_ = mode;
+		std::string &s = (*x.part)[t].s;
 		s.clear();
 		for (uint32_t k = lo; k < hi; k++) {
-			const uint64_t d = x.desc[k];
+			const uint64_t d = desc[k];
+			const uint8_t *const pkt = frames + NSD_DESC_OFF(d);
+			const uint32_t caplen = (uint32_t)NSD_DESC_CAPLEN(d);
 			// show_frame_hdr, then the entry point (netsniff-ng.c:732-737)
-			nsd::format_frame_hdr(s, x.fh[k], x.sll + k, x.frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), lt, mode,
-					      x.count0 + k);
+			nsd::format_frame_hdr(s, fh[k], sll + k, pkt, caplen, lt_, mode_, count0 + k);
 			const size_t mark = s.size();
-			const int r = nsd::format_packet_compact(s, x.frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), lt, mode,
-								 x.rec[k], k, x.ext, x.sll + k);
+			const int r = nsd::format_packet_compact(s, pkt, caplen, lt_, mode_, rec[k], k, ext, sll + k);
 			if (r == NSD_OK)
 				continue;
 			// a record that could not hold its chain (NSD_F_OVERFLOW: longer
 			// than NSD_EXT_MAX_LAYERS layers, or the ext pool was full) is
 			// rendered by the per-packet path, which has no layer budget;
 			// any other status is an error
-			if (!(x.rec[k].nflags & NSD_F_OVERFLOW))
+			if (!(rec[k].nflags & NSD_F_OVERFLOW))
 				return NSD_ERR_FORMAT;
 			s.resize(mark);
-			const int r2 = nsd::render_packet_cpu(s, x.frames + NSD_DESC_OFF(d), NSD_DESC_CAPLEN(d), lt, mode,
-							      x.sll + k);
+			const int r2 = nsd::render_packet_cpu(s, pkt, caplen, lt_, mode_, sll + k);
 			if (r2 != NSD_OK)
 				return r2;
 		}
 		return NSD_OK;
 	};
+	// copy job `q` of `parts` of a mapped file's batch
+	auto fill_part = [&](Slot &x, int q, int parts) {
+		const uint32_t lo = (uint32_t)((uint64_t)x.n * q / parts), hi = (uint32_t)((uint64_t)x.n * (q + 1) / parts);
+		fill_range(p, x.frames, x.desc, x.src, lo, hi, x.sll, x.fh, x.rhdr);
+	};
+	// the copy of a scanned batch (x.n records in slot k): parts 1.. on the
+	// pool, ahead of its render jobs, part 0 and whatever is left here
+	auto fill_batch = [&](Slot &x, int k) {
+		const int parts = x.n < 4096 ? 1 : (int)std::min<uint32_t>((uint32_t)threads + 1, x.n / 2048);
+		std::unique_lock<std::mutex> lk(mu);
+		x.fill_left = parts - 1;
+		for (int q = parts - 1; q >= 1; q--)
+			jobs.push_front({ k, q, parts });
+		if (parts > 1)
+			cv_job.notify_all();
+		lk.unlock();
+		fill_part(x, 0, parts);
+		lk.lock();
+		while (x.fill_left > 0) {
+			if (!jobs.empty() && jobs.front().parts > 0 && jobs.front().slot == k) {
+				const Job j = jobs.front();
+				jobs.pop_front();
+				lk.unlock();
+				fill_part(x, j.part, j.parts);
+				lk.lock();
+				x.fill_left--;
+				continue;
+			}
+			cv_fill.wait(lk);
+		}
+	};
 	std::vector<std::thread> pool;
+	const std::vector<int> cpus = pool_cpus();
 	for (int t = 0; t < threads; t++)
-		pool.emplace_back([&]() {
+		pool.emplace_back([&, t]() {
+			if (!cpus.empty()) {
+				// one formatter per physical core, near the caller; the
+				// caller's own core (the reader) is left out while others remain
+				cpu_set_t one;
+				CPU_ZERO(&one);
+				const size_t k = cpus.size() > 1 ? 1 + (size_t)t % (cpus.size() - 1) : 0;
+				CPU_SET(cpus[k], &one);
+				(void)pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+			}
 			std::unique_lock<std::mutex> lk(mu);
 			for (;;) {
 				cv_job.wait(lk, [&] { return stop || !jobs.empty(); });
 				if (jobs.empty())
 					return;
-				const auto j = jobs.front();
+				const Job j = jobs.front();
 				jobs.pop_front();
 				lk.unlock();
-				const long r = render(b[j.first], j.second);
+				if (j.parts > 0) {
+					fill_part(b[j.slot], j.part, j.parts);
+					lk.lock();
+					if (--b[j.slot].fill_left == 0)
+						cv_fill.notify_all();
+					continue;
+				}
+				const uint64_t t0 = stats ? ReplayStats::now() : 0;
+				const long r = render(b[j.slot], j.part);
+				if (stats) {
+					st.fmt += ReplayStats::now() - t0;
+					st.jobs++;
+				}
 				lk.lock();
-				Slot &x = b[j.first];
+				Slot &x = b[j.slot];
 				if (r != NSD_OK && x.prc == NSD_OK)
 					x.prc = r;
 				if (--x.left == 0)
@@ -689,10 +947,13 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			long r = x.prc;
 			const bool skip = err != NSD_OK;
 			lk.unlock();
+			const uint64_t t0 = stats ? ReplayStats::now() : 0;
 			if (!skip && r == NSD_OK)
 				r = put_parts(x);
 			if (!skip && r == NSD_OK)
 				r = put_records(x);
+			if (stats)
+				st.write += ReplayStats::now() - t0;
 			lk.lock();
 			if (r != NSD_OK && err == NSD_OK)
 				err = r;
@@ -710,8 +971,11 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		const int k = on_device.front();
 		on_device.pop_front();
 		Slot &x = b[k];
-		const int st = nsd_pipe_wait(pipe);
-		long r = st != NSD_OK ? (st < 0 ? st : NSD_ERR_HIP) : x.status;
+		const uint64_t t0 = stats ? ReplayStats::now() : 0;
+		const int ws = nsd_pipe_wait(pipe);
+		if (stats)
+			st.dev += ReplayStats::now() - t0;
+		long r = ws != NSD_OK ? (ws < 0 ? ws : NSD_ERR_HIP) : x.status;
 		if (r == NSD_OK && counters)
 			for (int c = 0; c < NSD_NCOUNTERS; c++)
 				counters[c] += x.cnt[c];
@@ -723,7 +987,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		to_write.push_back(k);
 		if (r == NSD_OK) {
 			for (int t = 0; t < x.parts; t++)
-				jobs.emplace_back(k, t);
+				jobs.push_back({ k, t, 0 });
 			cv_job.notify_all();
 		} else {
 			x.left = 0;
@@ -793,7 +1057,10 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 					continue;
 				}
 				lk.lock();
+				const uint64_t t0 = stats ? ReplayStats::now() : 0;
 				cv_free.wait(lk, [&] { return !free_slots.empty(); });
+				if (stats)
+					st.slot += ReplayStats::now() - t0;
 			}
 			k = free_slots.back();
 			free_slots.pop_back();
@@ -803,7 +1070,21 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			std::lock_guard<std::mutex> g(mu);
 			free_slots.push_back(k);
 		};
-		long n = read_batch(p, x.frames, FRAME_BYTES, x.desc, x.sll, x.fh, BATCH, nullptr, nullptr, x.rhdr);
+		const uint64_t tr = stats ? ReplayStats::now() : 0;
+		long n;
+		if (p->map) {
+			size_t end = 0;
+			n = scan_batch(p, FRAME_BYTES, x.desc, x.src, BATCH, &end);
+			if (n > 0) {
+				x.n = (uint32_t)n;
+				fill_batch(x, k);
+				memset(x.frames + end, 0, NSD_FRAME_PAD);
+			}
+		} else {
+			n = read_batch(p, x.frames, FRAME_BYTES, x.desc, x.sll, x.fh, BATCH, nullptr, nullptr, x.rhdr);
+		}
+		if (stats)
+			st.read += ReplayStats::now() - tr;
 		if (n == NSD_ERR_CAPLEN) {
 			give_back();
 			rc = one_big();
@@ -873,6 +1154,12 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	for (auto &t : pool)
 		t.join();
 	writer.join();
+	if (stats)
+		fprintf(stderr,
+			"nsd_replay: %ld records, %d threads, %.1f ms: read %.1f, device waits %.1f, slot waits %.1f, "
+			"format %.1f (%llu jobs, %.1f per thread), write %.1f ms\n",
+			printed, threads, (ReplayStats::now() - t_start) / 1e6, st.read / 1e6, st.dev / 1e6, st.slot / 1e6,
+			st.fmt / 1e6, (unsigned long long)st.jobs.load(), st.fmt / 1e6 / threads, st.write / 1e6);
 	// (an error leaves batches in the pipe: drop the cached set then)
 	if (&res == &own || rc != NSD_OK)
 		res.release();

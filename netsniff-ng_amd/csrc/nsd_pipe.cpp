@@ -30,6 +30,25 @@ bool ok(hipError_t e, const char *what)
 	return true;
 }
 
+// makes the pipe's device current for a scope (a caller that switched device
+// since the pipe was created still runs the pipe's batches where its buffers
+// are, and the launch's per-device schedule state is the pipe's device's)
+struct OnDevice {
+	int prev = -1;
+	explicit OnDevice(int dev)
+	{
+		if (hipGetDevice(&prev) != hipSuccess || prev == dev)
+			prev = -1;
+		else if (hipSetDevice(dev) != hipSuccess)
+			prev = -1;
+	}
+	~OnDevice()
+	{
+		if (prev >= 0)
+			(void)hipSetDevice(prev);
+	}
+};
+
 struct Slot {
 	hipStream_t stream = nullptr;
 	hipEvent_t done = nullptr;
@@ -60,6 +79,7 @@ struct nsd_pipe {
 	int depth = 0;
 	int start_id = 0;
 	int mode = 0;
+	int device = 0;         // the device current at creation: its streams and buffers
 	bool compact = false;   // nsd_crec records (nsd_pipe_create_compact)
 	int head = 0;    // oldest in flight
 	int count = 0;   // in flight
@@ -85,6 +105,7 @@ extern "C" void nsd_pipe_destroy(nsd_pipe *p)
 {
 	if (!p)
 		return;
+	const OnDevice on(p->device);
 	nsd_pipe_drain(p);
 	for (int k = 0; k < p->depth; k++)
 		slot_free(p->slot[k]);
@@ -115,7 +136,11 @@ static nsd_pipe *pipe_create(uint32_t max_pkts, size_t max_frame_bytes, uint32_t
 	int ndev = 0;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
 		return nullptr;
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess)
+		return nullptr;
 	nsd_pipe *p = new nsd_pipe;
+	p->device = dev;
 	p->max_pkts = max_pkts;
 	p->max_bytes = max_frame_bytes;
 	p->ext_cap = ext_cap;
@@ -183,6 +208,7 @@ extern "C" int nsd_pipe_wait(nsd_pipe *p)
 		return NSD_ERR_ARG;
 	if (!p->count)
 		return 1;
+	const OnDevice on(p->device);
 	return complete_oldest(p);
 }
 
@@ -190,6 +216,7 @@ extern "C" int nsd_pipe_drain(nsd_pipe *p)
 {
 	if (!p)
 		return NSD_ERR_ARG;
+	const OnDevice on(p->device);
 	int st = NSD_OK;
 	while (p->count) {
 		int r = complete_oldest(p);
@@ -240,6 +267,7 @@ static int pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len, co
 		return NSD_ERR_ARG;
 	if (n > p->max_pkts || frames_len > p->max_bytes)
 		return NSD_ERR_ARG;
+	const OnDevice on(p->device);
 	for (uint32_t i = 0; i < n; i++) {
 		const uint64_t cap = NSD_DESC_CAPLEN(desc[i]);
 		if (cap > NSD_MAX_CAPLEN)
@@ -284,11 +312,17 @@ static int pipe_submit(nsd_pipe *p, const uint8_t *frames, size_t frames_len, co
 }
 
 // point an idle pipe at another link type / print mode (the pcap replay keeps
-// one pipe for the process, nsd_pcap.cpp)
+// one pipe for the process, nsd_pcap.cpp); 1 when the pipe lives on another
+// device than the current one (the replay then builds a set on this one)
 extern "C" __attribute__((visibility("hidden"))) int nsd_pipe_retarget(nsd_pipe *p, int linktype, int mode)
 {
 	if (!p || p->count || mode < PRINT_NORM || mode > PRINT_NONE)
 		return NSD_ERR_ARG;
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess)
+		return NSD_ERR_HIP;
+	if (dev != p->device)
+		return 1;
 	p->start_id = nsd_start_for(linktype);
 	p->mode = mode;
 	return NSD_OK;

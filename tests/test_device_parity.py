@@ -433,3 +433,39 @@ def test_plain_tiles(mode, align):
     frames, desc = T.batch_from_packets(_plain_tiles(), align=align)
     _check(frames, desc, mode)
     _check_compact(frames, desc, mode)
+
+
+def _not_plain(rnd, pkt):
+    """One frame the plain path must refuse, made from a plain one: IHL 6
+    (an options word), an 802.1Q tag, ICMP, or a frame one byte too short."""
+    kind = rnd.randrange(4)
+    if kind == 0:
+        ip = bytearray(pkt[14:34])
+        ip[0] = 0x46
+        return pkt[:14] + bytes(ip) + b"\x01\x01\x01\x00" + pkt[34:]
+    if kind == 1:
+        return pkt[:12] + b"\x81\x00\x00\x05" + pkt[12:]
+    if kind == 2:
+        return pkt[:23] + b"\x01" + pkt[24:]
+    return pkt[:41]
+
+
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_plain_tiles_partial_and_mixed(mode):
+    """The plain path's wave-level edges: a partial last tile (64 * 48 + 17
+    frames: invalid lanes with clamped descriptors stay out of the ballot),
+    and tiles of plain frames where one random lane holds a frame that is not
+    plain (the whole tile then goes through fast_walk); both record forms,
+    under both schedules (the module's schedule fixture)."""
+    import random
+    rnd = random.Random(23)
+    pkts = _plain_tiles(seed=5, n=64 * 48 + 17)
+    frames, desc = T.batch_from_packets(pkts, align=2)
+    _check(frames, desc, mode)
+    _check_compact(frames, desc, mode)
+    for t in range(0, 48, 3):   # one non-plain lane in every third tile
+        k = 64 * t + rnd.randrange(64)
+        pkts[k] = _not_plain(rnd, pkts[k])
+    frames, desc = T.batch_from_packets(pkts, align=1)
+    _check(frames, desc, mode)
+    _check_compact(frames, desc, mode)
