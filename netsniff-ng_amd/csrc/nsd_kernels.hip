@@ -2013,7 +2013,12 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 		S.cus = cus;
 	}
 	Plan p{ false, false, false, S.cus };
-	if (S.pending && hipEventQuery(S.ev) == hipSuccess) {
+	// a launch captured into a graph takes the schedule as it stands and is
+	// never the sample (an event query or a host copy would break the
+	// capture; the graph replays this plan)
+	hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+	const bool capturing = hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+	if (!capturing && S.pending && hipEventQuery(S.ev) == hipSuccess) {
 		const double rd = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
 		const double ri = S.sampled ? (double)S.host[1] / (double)S.sampled : 0.0;
 		S.fused = S.fused ? rd > 0.05 || ri > 0.05 : rd > 0.15 || ri > 0.10;
@@ -2022,7 +2027,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 			S.small = by <= (uint64_t)NSD_SMALL_FRAME * pk;
 		S.pending = false;
 	}
-	if (!S.init) {
+	if (!S.init && !capturing) {
 		S.init = true;
 		if (hipHostMalloc((void **)&S.host, 64, hipHostMallocDefault) != hipSuccess ||
 		    hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess)
@@ -2030,7 +2035,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 	}
 	p.fused = g_sched_force ? g_sched_force == NSD_SCHED_FUSED : S.fused;
 	p.small = S.small;
-	if (++S.launches >= NSD_SCHED_SAMPLE && !S.pending && S.host && pair && counters &&
+	if (!capturing && ++S.launches >= NSD_SCHED_SAMPLE && !S.pending && S.host && pair && counters &&
 	    hipMemsetAsync(pair, 0, 16, stream) == hipSuccess &&
 	    hipMemcpyAsync(S.host + 2, counters + NSD_CNT_PKTS, 16, hipMemcpyDeviceToHost, stream) == hipSuccess) {
 		p.sample = true;

@@ -92,8 +92,12 @@ def _check_compact(frames, desc, mode):
     d = torch.from_numpy(desc.view(np.int64)).cuda()
     crec, ext, used, cnt = nsd.dissect_device_compact(f, d, mode=mode)
     torch.cuda.synchronize()
+    return _compare_compact(crec, ext, used, cnt, frames, desc, mode)
+
+
+def _compare_compact(crec, ext, used, cnt, frames, desc, mode):
     n = len(desc)
-    got = crec.cpu().numpy().view(nsd.CREC_DTYPE)
+    got = crec.cpu().numpy().view(nsd.CREC_DTYPE)[:n]
     dpool = ext.cpu().numpy().view(np.uint32)[:n + int(used.item())]
     orec, oext, ocnt, _ = T.oracle_records(frames, desc, mode=mode)
     want, wpool = nsd.compact_of(orec, oext)
@@ -469,3 +473,67 @@ def test_plain_tiles_partial_and_mixed(mode):
     frames, desc = T.batch_from_packets(pkts, align=1)
     _check(frames, desc, mode)
     _check_compact(frames, desc, mode)
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_graph_capture_and_replay(compact, schedule):
+    """nsd_dissect_device_ws / _compact captured into a HIP graph (torch.cuda
+    graph on the launch stream): the walk of a fixed-size batch replayed
+    over new frames in the same buffers gives the oracle's records and
+    counters each time (C2, C3, C4 batches through one graph), under both
+    schedules (an adaptive launch under capture keeps the plan it has and is
+    never the sample: no event query or host copy inside the graph)."""
+    import torch
+    n = 8192
+    batches = [T.make_batch(cfg, n, seed=T.SEED + k) for k, cfg in
+               enumerate((T.SYN_UDP64, T.SYN_IMIX, T.SYN_IPV6X, T.SYN_IMIX))]
+    cap = max(len(f) for f, _ in batches)
+    dev = torch.device("cuda", 0)
+    frames = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    desc = torch.zeros(n, dtype=torch.int64, device=dev)
+    rb = nsd.CREC_BYTES if compact else nsd.REC_BYTES
+    rec = torch.empty(n * rb, dtype=torch.uint8, device=dev)
+    ext = torch.empty(nsd.ext_pool_words(n), dtype=torch.int32, device=dev)
+    used = torch.zeros(1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device=dev)
+    ws = torch.empty(nsd.lib().nsd_workspace_bytes(n), dtype=torch.uint8, device=dev)
+
+    def walk():
+        used.zero_()
+        cnt.zero_()
+        if compact:
+            nsd.dissect_device_compact(frames, desc, mode=T.PRINT_NORM, crec=rec, ext=ext, ext_used=used,
+                                       counters=cnt, workspace=ws)
+        else:
+            nsd.dissect_device(frames, desc, mode=T.PRINT_NORM, rec=rec, ext=ext, ext_used=used, counters=cnt,
+                               workspace=ws)
+
+    def load(k):
+        f, d = batches[k]
+        frames.zero_()
+        frames[:len(f)].copy_(torch.from_numpy(f))
+        desc.copy_(torch.from_numpy(d.view(np.int64)))
+
+    load(0)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        walk()   # warm-up outside the capture (occupancy queries, first-use state)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        walk()
+    for k in range(len(batches)):
+        load(k)
+        g.replay()
+        torch.cuda.synchronize()
+        f, d = batches[k]
+        if compact:
+            _compare_compact(rec, ext, used, cnt, f, d, T.PRINT_NORM)
+        else:
+            drec = rec.cpu().numpy().view(nsd.REC_DTYPE)
+            dext = ext.cpu().numpy().view(np.uint32)[:int(used.item())]
+            orec, oext, ocnt, _ = T.oracle_records(f, d, mode=T.PRINT_NORM)
+            assert_same_records(drec, orec, dext, oext)
+            assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt)

@@ -129,6 +129,50 @@ def test_reader_batches_and_end_rules(tmp_path):
         nsd.pcap_read(bad)
 
 
+def _fifo_feed(path, data):
+    """A named pipe at `path` that a thread fills with `data` (the reader's
+    read() path: a non-regular file is not mapped)."""
+    import threading
+    os.mkfifo(path)
+
+    def feed():
+        with open(path, "wb") as f:
+            f.write(data)
+    t = threading.Thread(target=feed, daemon=True)
+    t.start()
+    return t
+
+
+def test_reader_mapped_and_read_paths_agree(tmp_path, monkeypatch):
+    """A regular file is mapped, anything else read with read() (or any file
+    with NSD_PCAP_MMAP=0): the same records, frame header fields and
+    sockaddr_ll from both, including the end rules (a zero-length record, a
+    truncated last record) and a named pipe."""
+    pkts = [p for p in T.read_pcap(os.path.join(G, "edge.pcap"))[1] if p]
+    full = str(tmp_path / "full.pcap")
+    T.write_pcap(full, pkts)
+    z = str(tmp_path / "z.pcap")
+    rewrite(pkts[:5] + [b""] + pkts[5:9], z)
+    t = str(tmp_path / "t.pcap")
+    open(t, "wb").write(open(full, "rb").read()[:-3])
+    files = [full, z, t] + [os.path.join(G, f) for f in sorted(os.listdir(G)) if f.startswith("fh_") and
+                            f.endswith(".pcap")]
+    for f in files:
+        mapped = nsd.pcap_frame_hdrs(f)
+        monkeypatch.setenv("NSD_PCAP_MMAP", "0")
+        read = nsd.pcap_frame_hdrs(f)
+        monkeypatch.delenv("NSD_PCAP_MMAP")
+        assert mapped[0] == read[0] and mapped[1] == read[1], f
+        assert np.array_equal(mapped[2], read[2]) and np.array_equal(mapped[3], read[3]), f
+        assert packets_of(f, cap=4096, max_n=7)[1] == mapped[1]
+    fifo = str(tmp_path / "p.pcap")
+    th = _fifo_feed(fifo, open(full, "rb").read())
+    got = nsd.pcap_frame_hdrs(fifo)
+    th.join(10)
+    ref = nsd.pcap_frame_hdrs(full)
+    assert got[1] == ref[1] and np.array_equal(got[2], ref[2])
+
+
 MODES = [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX, T.PRINT_ASCII, T.PRINT_HEX_ASCII]
 
 
@@ -171,6 +215,28 @@ def test_replay_edge_matches_golden(tmp_path, mode):
     fl = frame_lines(path, mode)
     assert text == b"".join(fl[k] + gold[i] for k, i in enumerate(keep))
     assert int(cnt[nsd.CNT_PKTS]) == len(keep)
+
+
+@pytest.mark.gpu
+def test_replay_read_paths(tmp_path, monkeypatch):
+    """The replay's two readers give the same text: the mapped file (header
+    scan on the reader, bodies copied by the pool, several pool sizes), the
+    read() path (NSD_PCAP_MMAP=0) and a named pipe."""
+    path, keep = replayable("edge", T.PRINT_NORM, tmp_path)
+    pkts = [p for p in T.read_pcap(path)[1]]
+    big = str(tmp_path / "big.pcap")
+    T.write_pcap(big, pkts * 600)   # > one 65536-record batch
+    for pth in (path, big):
+        n0, ref = nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=1)
+        for th in (2, 5, 16):
+            assert nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=th) == (n0, ref)
+        monkeypatch.setenv("NSD_PCAP_MMAP", "0")
+        assert nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=4) == (n0, ref)
+        monkeypatch.delenv("NSD_PCAP_MMAP")
+    fifo = str(tmp_path / "p.pcap")
+    t = _fifo_feed(fifo, open(big, "rb").read())
+    assert nsd.replay_pcap(fifo, mode=T.PRINT_NORM, threads=4) == (n0, ref)
+    t.join(10)
 
 
 @pytest.mark.gpu
