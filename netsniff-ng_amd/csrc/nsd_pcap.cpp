@@ -572,6 +572,48 @@ ReplayRes g_replay;
 // sibling formats at a fraction of a core's rate), those of the calling
 // thread's NUMA node first, of the CPUs this process may use.  Empty when
 // the topology cannot be read (then nothing is pinned), or NSD_REPLAY_PIN=0.
+// The topology is read from /sys once per process.
+struct CpuTopo {
+	int cpu;
+	long pkg, core;
+	int node;
+};
+const std::vector<CpuTopo> &cpu_topology()
+{
+	static const std::vector<CpuTopo> topo = [] {
+		std::vector<CpuTopo> t;
+		auto rd = [](int cpu, const char *what) -> long {
+			char path[128];
+			snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/%s", cpu, what);
+			FILE *f = fopen(path, "r");
+			if (!f)
+				return -1;
+			long v = -1;
+			if (fscanf(f, "%ld", &v) != 1)
+				v = -1;
+			fclose(f);
+			return v;
+		};
+		for (int c = 0; c < CPU_SETSIZE; c++) {
+			const long pkg = rd(c, "topology/physical_package_id"), core = rd(c, "topology/core_id");
+			if (pkg < 0 || core < 0)
+				continue;
+			int node = 0;
+			for (int n = 0; n < 64; n++) {
+				char path[128];
+				snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/node%d", c, n);
+				if (access(path, F_OK) == 0) {
+					node = n;
+					break;
+				}
+			}
+			t.push_back({ c, pkg, core, node });
+		}
+		return t;
+	}();
+	return topo;
+}
+
 std::vector<int> pool_cpus()
 {
 	std::vector<int> out;
@@ -581,56 +623,34 @@ std::vector<int> pool_cpus()
 	cpu_set_t set;
 	if (sched_getaffinity(0, sizeof(set), &set) != 0)
 		return out;
-	auto rd = [](int cpu, const char *what) -> long {
-		char path[128];
-		snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/%s", cpu, what);
-		FILE *f = fopen(path, "r");
-		if (!f)
-			return -1;
-		long v = -1;
-		if (fscanf(f, "%ld", &v) != 1)
-			v = -1;
-		fclose(f);
-		return v;
-	};
-	auto node_of = [](int cpu) -> int {
-		for (int n = 0; n < 64; n++) {
-			char path[128];
-			snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/node%d", cpu, n);
-			if (access(path, F_OK) == 0)
-				return n;
-		}
-		return 0;
-	};
+	const std::vector<CpuTopo> &topo = cpu_topology();
 	const int me = sched_getcpu();
-	const int my_node = me >= 0 ? node_of(me) : 0;
+	const CpuTopo *mine = nullptr;
+	for (const CpuTopo &t : topo)
+		if (t.cpu == me)
+			mine = &t;
 	std::vector<std::pair<long, long>> seen;   // (package, core)
 	std::vector<int> near, far;
-	for (int c = 0; c < CPU_SETSIZE; c++) {
-		if (!CPU_ISSET(c, &set))
+	int first = -1;                            // the caller's core
+	for (const CpuTopo &t : topo) {
+		if (!CPU_ISSET(t.cpu, &set))
 			continue;
-		const long pkg = rd(c, "topology/physical_package_id"), core = rd(c, "topology/core_id");
-		if (pkg < 0 || core < 0)
-			return {};
 		bool dup = false;
 		for (auto &x : seen)
-			dup = dup || (x.first == pkg && x.second == core);
+			dup = dup || (x.first == t.pkg && x.second == t.core);
 		if (dup)
 			continue;
-		seen.emplace_back(pkg, core);
-		(node_of(c) == my_node ? near : far).push_back(c);
+		seen.emplace_back(t.pkg, t.core);
+		if (mine && t.pkg == mine->pkg && t.core == mine->core)
+			first = t.cpu;
+		else
+			(!mine || t.node == mine->node ? near : far).push_back(t.cpu);
 	}
-	out = near;
-	out.insert(out.end(), far.begin(), far.end());
 	// the caller's core first (the pool leaves it to the reader)
-	if (me >= 0) {
-		const long mp = rd(me, "topology/physical_package_id"), mc = rd(me, "topology/core_id");
-		for (size_t k = 0; k < out.size(); k++)
-			if (rd(out[k], "topology/physical_package_id") == mp && rd(out[k], "topology/core_id") == mc) {
-				std::swap(out[0], out[k]);
-				break;
-			}
-	}
+	if (first >= 0)
+		out.push_back(first);
+	out.insert(out.end(), near.begin(), near.end());
+	out.insert(out.end(), far.begin(), far.end());
 	return out;
 }
 
