@@ -101,12 +101,34 @@ __device__ __forceinline__ uint32_t pkt_load(const uint8_t *p, uint32_t off, uin
 	return size == 4 ? be : size == 2 ? be >> 16 : be >> 24;
 }
 
+// Each packet's first 64 bytes, from the 16-byte aligned address at or
+// below its start, are staged in LDS before the program runs: a wave's 64
+// frames are fetched by four coalesced 16-byte loads per lane (lane L loads
+// chunk L & 3 of packet 16 t + L / 4), so a header filter's loads are LDS
+// reads instead of a chain of dependent HBM loads per instruction.  A row is
+// 16 dwords; chunk c of packet q sits in slot c ^ (q & 3) (lanes reading one
+// header offset spread over the banks).  Loads that reach past the row read
+// the frame in HBM (pkt_load).
+constexpr uint32_t ROWW = 16;
+
+// big-endian `size`-byte value at row position r (r + size <= 64)
+__device__ __forceinline__ uint32_t row_load(const uint32_t *row, uint32_t sw, uint32_t r, uint32_t size)
+{
+	const uint32_t j = r >> 2;
+	// (when j + 1 is 16 the bytes lie in dword j alone: the other word is any)
+	const uint32_t v = __builtin_amdgcn_alignbyte(row[((j + 1) & 15) ^ sw], row[j ^ sw], r & 3);
+	const uint32_t be = __builtin_bswap32(v);
+	return size == 4 ? be : size == 2 ? be >> 16 : be >> 24;
+}
+
 // bpf_run_filter (bpf.c:508-705) for one packet per lane.  Every program the
 // loader accepts jumps forward only, so it retires within `len` steps; the
 // step bound is the loop's exit condition regardless.  mem: this lane's
-// scratch words M[j] at mem[j * BLOCK].
+// scratch words M[j] at mem[j * BLOCK]; row / sw / m: the staged first bytes
+// (row position = packet offset + m).
 __device__ __forceinline__ uint32_t run_one(const uint2 *prog, uint32_t len, uint32_t *mem,
-					    bool usesmem, const uint8_t *p, uint32_t plen, bool on)
+					    bool usesmem, const uint8_t *p, uint32_t plen, bool on,
+					    const uint32_t *row, uint32_t sw, uint32_t m)
 {
 	if (usesmem)
 		for (uint32_t j = 0; j < MEMWORDS; j++)
@@ -132,7 +154,8 @@ __device__ __forceinline__ uint32_t run_one(const uint2 *prog, uint32_t len, uin
 				ret = 0;
 				run = false;
 			} else {
-				A = pkt_load(p, off, size);
+				const uint32_t r = off + m;   // (off < plen <= 65535)
+				A = r + size <= 4 * ROWW ? row_load(row, sw, r, size) : pkt_load(p, off, size);
 			}
 			break;
 		}
@@ -141,7 +164,8 @@ __device__ __forceinline__ uint32_t run_one(const uint2 *prog, uint32_t len, uin
 				ret = 0;
 				run = false;
 			} else {
-				X = (pkt_load(p, k, 1) & 0xf) << 2;
+				const uint32_t r = k + m;
+				X = ((r < 4 * ROWW ? row_load(row, sw, r, 1) : pkt_load(p, k, 1)) & 0xf) << 2;
 			}
 			break;
 		case K_LEN: if (fx) X = plen; else A = plen; break;
@@ -180,6 +204,25 @@ __device__ __forceinline__ uint32_t run_one(const uint2 *prog, uint32_t len, uin
 	return run ? 0u : ret;
 }
 
+typedef uint32_t bv4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const bv4u gbv4u;
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// dynamic LDS of a bpf_filter block: the program, the staged rows, and the
+// scratch words when the program uses them
+__host__ __device__ constexpr size_t prog_bytes(uint32_t len) { return ((size_t)len * 8 + 15) & ~(size_t)15; }
+__host__ __device__ constexpr size_t filter_lds(uint32_t len, bool usesmem)
+{
+	return prog_bytes(len) + (size_t)BLOCK * ROWW * 4 + (usesmem ? (size_t)MEMWORDS * BLOCK * 4 : 0);
+}
+static_assert(filter_lds(MAXINSNS, true) <= 65536, "a bpf_filter block's LDS");
+
 // One tile of TILE packets per block: verdicts, and the tile's accepted
 // count when compacting.
 template <bool COUNT>
@@ -188,12 +231,18 @@ __global__ __launch_bounds__(BLOCK) void bpf_filter(const uint2 *__restrict__ gp
 						    const uint64_t *__restrict__ desc, uint32_t n,
 						    uint32_t *__restrict__ verdict, uint32_t *__restrict__ tile_cnt)
 {
-	extern __shared__ uint2 prog[];
-	__shared__ uint32_t mem[MEMWORDS * BLOCK];
-	__shared__ uint32_t wcnt[WAVES];
+	extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+	uint2 *const prog = (uint2 *)lds;
+	uint32_t *const rows = (uint32_t *)(lds + prog_bytes(len));
+	uint32_t *const mem = rows + BLOCK * ROWW;
+	uint32_t *const wcnt = rows;   // (after the rounds; the largest program fills 64 KiB exactly)
 	for (uint32_t j = threadIdx.x; j < len; j += BLOCK)
 		prog[j] = gprog[j];
 	__syncthreads();
+	const uint32_t lane = threadIdx.x & 63;
+	uint32_t *const wrows = rows + (threadIdx.x & ~63u) * ROWW;
+	const uint32_t *const row = wrows + lane * ROWW;
+	const uint32_t sw = (lane & 3) << 2;
 	uint32_t acc = 0;
 	const uint64_t base = (uint64_t)blockIdx.x * TILE;
 #pragma unroll 1
@@ -201,16 +250,32 @@ __global__ __launch_bounds__(BLOCK) void bpf_filter(const uint2 *__restrict__ gp
 		const uint64_t i = base + r * BLOCK + threadIdx.x;
 		const bool on = i < n;
 		const uint64_t d = on ? desc[i] : 0;
-		const uint32_t v = run_one(prog, len, mem + threadIdx.x, usesmem != 0, frames + NSD_DESC_OFF(d),
-					   NSD_DESC_CAPLEN(d), on);
+		const uint64_t a = (uint64_t)(uintptr_t)frames + NSD_DESC_OFF(d);
+		// the wave's 64 first windows (past the batch: frames[0, 64), readable)
+		bv4u v[4];
+#pragma unroll
+		for (uint32_t t = 0; t < 4; t++) {
+			const int q = (int)(16 * t + (lane >> 2));
+			const uint64_t aq = (uint64_t)__shfl((uint32_t)a, q, 64) | (uint64_t)__shfl((uint32_t)(a >> 32), q, 64) << 32;
+			v[t] = __builtin_nontemporal_load((gbv4u *)(uintptr_t)((aq & ~15ull) + 16 * (lane & 3)));
+		}
+		wave_lds_sync();   // (the previous round's reads of the rows are done)
+#pragma unroll
+		for (uint32_t t = 0; t < 4; t++) {
+			const uint32_t q = 16 * t + (lane >> 2);
+			*(bv4u *)(wrows + q * ROWW + (((lane & 3) ^ (q & 3)) << 2)) = v[t];
+		}
+		wave_lds_sync();
+		const uint32_t vd = run_one(prog, len, mem + threadIdx.x, usesmem != 0, frames + NSD_DESC_OFF(d),
+					    NSD_DESC_CAPLEN(d), on, row, sw, (uint32_t)(a & 15));
 		if (on)
-			verdict[i] = v;
-		acc += (on && v != 0) ? 1u : 0u;
+			verdict[i] = vd;
+		acc += (on && vd != 0) ? 1u : 0u;
 	}
 	if (COUNT) {
-		const uint32_t lane = threadIdx.x & 63;
 		for (int s = 32; s; s >>= 1)
 			acc += __shfl_xor(acc, s, 64);
+		__syncthreads();   // every wave is done with its rows
 		if (lane == 0)
 			wcnt[threadIdx.x >> 6] = acc;
 		__syncthreads();
@@ -447,7 +512,7 @@ extern "C" int nsd_bpf_filter_device(const nsd_bpf_prog *prog, const uint8_t *d_
 	}
 	const uint32_t tiles = tiles_for(n);
 	uint32_t *tile_cnt = (uint32_t *)d_workspace;
-	const size_t lds = (size_t)prog->len * sizeof(uint2);
+	const size_t lds = filter_lds(prog->len, prog->usesmem != 0);
 	if (compact) {
 		hipLaunchKernelGGL(bpf_filter<true>, dim3(tiles), dim3(BLOCK), lds, s, prog->d_prog, prog->len,
 				   prog->usesmem, d_frames, (const uint64_t *)d_desc, n, d_verdict, tile_cnt);

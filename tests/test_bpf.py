@@ -395,3 +395,33 @@ def test_device_filter_then_dissect():
     for fld in ("chain", "data_off", "tail_off", "ip_csum", "nflags"):
         assert np.array_equal(drec[fld], orec[fld]), fld
     assert np.array_equal(counters.cpu().numpy().view(np.uint64), ocnt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("usesmem", [False, True])
+def test_device_largest_program(usesmem):
+    """A program of BPF_MAXINSNS (4096) instructions, with and without the
+    scratch words (the largest LDS the filter block takes): packet loads at
+    every offset around the staged 64-byte window's end (and past it), so
+    the staged and the HBM loads meet in one program; verdicts equal the
+    oracle's at alignments 1 and 16."""
+    rnd = random.Random(13)
+    ins = []
+    while len(ins) < 4095:
+        k = rnd.choice([rnd.randrange(56, 72), rnd.randrange(0, 64), rnd.randrange(64, 300)])
+        ins.append((rnd.choice([0x20, 0x28, 0x30]), 0, 0, k))        # ld [k]
+        if usesmem:
+            j = rnd.randrange(16)
+            ins.append((0x02, 0, 0, j))                              # st M[j]
+            ins.append((0x61, 0, 0, j))                              # ldx M[j]
+        else:
+            ins.append((0x07, 0, 0, 0))                              # tax
+        ins.append((0x0c, 0, 0, 0))                                  # add x
+    ins = ins[:4095]
+    ins.append((0x16, 0, 0, 0))                                      # ret a
+    p = prog(*ins)
+    assert len(p) == 4096 and nsd.bpf_validate(p) == 1
+    pkts = [bytes(rnd.randrange(256) for _ in range(rnd.choice([60, 64, 65, 70, 300, 1500]))) for _ in range(700)]
+    for align in (1, 16):
+        frames, desc = T.batch_from_packets(pkts, align=align)
+        assert np.array_equal(nsd.BpfProgram(p).filter_batch(frames, desc), oracle_batch(p, frames, desc))
