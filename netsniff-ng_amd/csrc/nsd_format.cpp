@@ -34,25 +34,61 @@ static const char C_BOLD[] = "\033[1m";
 static const char C_RED[] = "\033[30;41m";
 static const char C_END[] = "\033[0m";
 
+// The text sink: appends go to a small buffer on the stack and reach the
+// string a few KiB at a time (std::string::append per field costs a call and
+// a capacity check; a packet is ~80 fields).  One Out per string at a time:
+// its destructor flushes, so the string is complete when the entry returns.
 struct Out {
 	std::string &s;
-	explicit Out(std::string &str) : s(str) {}
-	Out &operator<<(const char *t) { s.append(t); return *this; }
-	Out &put(const char *t, size_t n) { s.append(t, n); return *this; }
-	Out &c(char ch) { s.push_back(ch); return *this; }
+	char *w;
+	char buf[4096];
+	explicit Out(std::string &str) : s(str), w(buf) {}
+	Out(const Out &) = delete;
+	Out &operator=(const Out &) = delete;
+	~Out() { flush(); }
+	void flush()
+	{
+		if (w != buf)
+			s.append(buf, (size_t)(w - buf));
+		w = buf;
+	}
+	// room for n <= sizeof(buf) bytes at w
+	char *room(size_t n)
+	{
+		if ((size_t)(buf + sizeof(buf) - w) < n)
+			flush();
+		return w;
+	}
+	Out &put(const char *t, size_t n)
+	{
+		if (n > sizeof(buf) / 2) {
+			flush();
+			s.append(t, n);
+			return *this;
+		}
+		memcpy(room(n), t, n);
+		w += n;
+		return *this;
+	}
+	Out &operator<<(const char *t) { return put(t, strlen(t)); }
+	Out &c(char ch)
+	{
+		*room(1) = ch;
+		w++;
+		return *this;
+	}
 	// %u
 	Out &u(uint64_t v)
 	{
 		char b[24];
 		int i = 24;
 		do { b[--i] = (char)('0' + v % 10); v /= 10; } while (v);
-		s.append(b + i, 24 - i);
-		return *this;
+		return put(b + i, (size_t)(24 - i));
 	}
 	// %d / %zd
 	Out &d(int64_t v)
 	{
-		if (v < 0) { s.push_back('-'); return u((uint64_t)(-(v + 1)) + 1); }
+		if (v < 0) { c('-'); return u((uint64_t)(-(v + 1)) + 1); }
 		return u((uint64_t)v);
 	}
 	// %x
@@ -62,8 +98,7 @@ struct Out {
 		char b[16];
 		int i = 16;
 		do { b[--i] = hx[v & 15]; v >>= 4; } while (v);
-		s.append(b + i, 16 - i);
-		return *this;
+		return put(b + i, (size_t)(16 - i));
 	}
 	// %.Nx (zero padded to at least N digits)
 	Out &xn(uint64_t v, int n)
@@ -73,8 +108,7 @@ struct Out {
 		int i = 16;
 		do { b[--i] = hx[v & 15]; v >>= 4; } while (v);
 		while (16 - i < n) b[--i] = '0';
-		s.append(b + i, 16 - i);
-		return *this;
+		return put(b + i, (size_t)(16 - i));
 	}
 };
 
@@ -151,12 +185,19 @@ static const char *ether_class(const Frame &f, uint32_t mac)
 	return v ? v : "Unknown";
 }
 
+// "%.2x:%.2x:%.2x:%.2x:%.2x:%.2x" in one write
 static void mac(Out &o, const Frame &f, uint32_t m)
 {
+	static const char hx[] = "0123456789abcdef";
+	char *w = o.room(17);
 	for (int i = 0; i < 6; i++) {
-		if (i) o.c(':');
-		o.xn(f.b(m + i), 2);
+		const uint8_t b = f.b(m + i);
+		if (i)
+			*w++ = ':';
+		*w++ = hx[b >> 4];
+		*w++ = hx[b & 15];
 	}
+	o.w = w;
 }
 
 // ---- layers --------------------------------------------------------------
@@ -900,11 +941,14 @@ static void dump_ascii(Out &o, const Frame &f, uint32_t from, uint32_t len)
 	if (!len)
 		return;
 	o << " [ Chr ";
-	size_t at = o.s.size();
-	o.s.resize(at + len);
-	for (uint32_t i = 0; i < len; i++) {
-		const uint8_t c = f.b(from + i);
-		o.s[at + i] = (c >= 0x20 && c < 0x7f) ? (char)c : '.';
+	for (uint32_t i0 = 0; i0 < len; i0 += 1024) {
+		const uint32_t m = len - i0 < 1024 ? len - i0 : 1024;
+		char *w = o.room(m);
+		for (uint32_t i = 0; i < m; i++) {
+			const uint8_t c = f.b(from + i0 + i);
+			w[i] = (c >= 0x20 && c < 0x7f) ? (char)c : '.';
+		}
+		o.w += m;
 	}
 	o << " ]\n";
 }
@@ -915,14 +959,16 @@ static void dump_hex(Out &o, const Frame &f, uint32_t from, uint32_t len)
 	if (!len)
 		return;
 	o << " [ Hex ";
-	size_t at = o.s.size();
-	o.s.resize(at + 3 * (size_t)len);
-	char *w = &o.s[at];
-	for (uint32_t i = 0; i < len; i++) {
-		const uint8_t c = f.b(from + i);
-		w[3 * i] = ' ';
-		w[3 * i + 1] = hx[c >> 4];
-		w[3 * i + 2] = hx[c & 15];
+	for (uint32_t i0 = 0; i0 < len; i0 += 512) {
+		const uint32_t m = len - i0 < 512 ? len - i0 : 512;
+		char *w = o.room(3 * (size_t)m);
+		for (uint32_t i = 0; i < m; i++) {
+			const uint8_t c = f.b(from + i0 + i);
+			w[3 * i] = ' ';
+			w[3 * i + 1] = hx[c >> 4];
+			w[3 * i + 2] = hx[c & 15];
+		}
+		o.w += 3 * (size_t)m;
 	}
 	o << " ]\n";
 }
