@@ -432,6 +432,32 @@ def cpu_rate(cfg, n_sample, threads, seconds, text):
     return done / dt / 1e6, done, dt
 
 
+def ref_harness_rate(cfg, key, n=1 << 17, frames=True):
+    """`netsniff-ng --in`'s loop through the reference's own objects on one
+    core: oracle/_ref/nsref (built here from /root/reference's sources: its
+    pcap reader and record conversion, parser objects and tprintf.c; the
+    IPv4/IPv6 layers are the restatement, their sources need config.h) over a
+    synthetic pcap of n records, text to /dev/null.  None when the harness
+    was not built."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "nsref")
+    if not os.path.exists(exe):
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "ref.pcap")
+        T.synth().nsd_synth_pcap(cfg, T.SEED, 0, n, path.encode())
+        t0 = time.perf_counter()
+        r = subprocess.run([exe] + (["-f"] if frames else []) +
+                           ["-m", str(T.PRINT_NORM), "-w", "65535", "-i", os.path.join(d, "idx"), path],
+                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
+        dt = time.perf_counter() - t0
+    if r.returncode != 0:
+        return None
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "reference",
+            "sample": f"{key}: {n} records, `nsref{' -f' if frames else ''}` "
+                      f"({'frame header line (if_indextoname per packet, as the reference) + ' if frames else ''}"
+                      f"dissector text, unwrapped) to /dev/null in {dt:.2f} s, process start included"}
+
+
 def cpu_baseline(key, seconds):
     """The CPU restatement on this host (SURVEY 8d / BASELINE.md "CPU-baseline
     plan"): fields + PRINT_NORM text and fields only, each on 1 thread, on
@@ -463,7 +489,9 @@ def cpu_baseline(key, seconds):
             "text_16threads": {"threads": t16, "value": round(tS, 3)},
             "fields_only": {"all_cores": round(fA, 3), "threads16": round(fS, 3), "1thread": round(f1, 3)},
             "reference_harness_container": "0.182 Mpkt/s PRINT_NORM 1 core (BASELINE.md, measured in the "
-                                           "build container, not on this host)"}
+                                           "build container, not on this host)",
+            "reference_harness_1thread": ref_harness_rate(cfg, key),
+            "reference_dissector_1thread": ref_harness_rate(cfg, key, frames=False)}
 
 
 # ---- host-memory legs (reported, never `value`) ----------------------------------------
