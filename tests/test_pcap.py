@@ -240,6 +240,33 @@ def test_replay_read_paths(tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_concurrent_replays(tmp_path):
+    """Two replays at once in one process (ctypes drops the GIL): one takes
+    the cached staging and device pipe, the other builds its own set; both
+    print exactly what a replay alone prints, and the next replay after them
+    too."""
+    import threading
+    path, keep = replayable("edge", T.PRINT_NORM, tmp_path)
+    pkts = [p for p in T.read_pcap(path)[1]]
+    big = str(tmp_path / "big.pcap")
+    T.write_pcap(big, pkts * 900)
+    want = {pth: nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=4) for pth in (path, big)}
+    got = {}
+
+    def run(k, pth):
+        got[k] = nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=4)
+
+    for _ in range(3):
+        ts = [threading.Thread(target=run, args=(k, pth)) for k, pth in enumerate((big, big, path))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        assert got[0] == want[big] and got[1] == want[big] and got[2] == want[path]
+    assert nsd.replay_pcap(big, mode=T.PRINT_NORM, threads=4) == want[big]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
 def test_replay_wrapped_and_filtered(tmp_path, mode):
     """80-column tprintf wrap over the replay stream, and a BPF filter in
