@@ -49,3 +49,47 @@ extern "C" int nsd_bw_read(const void *buf, size_t bytes, int blocks_per_cu, int
 		hipLaunchKernelGGL(k_read<false>, grid, dim3(256), 0, (hipStream_t)stream, (const v4u *)buf, n, sink);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// The fast walk's access shape alone: every packet's first 64 bytes (from
+// the 16-byte aligned address at or below its start) as four 16-byte loads
+// by four consecutive lanes, a wave per tile of 64 packets, one tile of
+// loads in flight per wave, plus the descriptor loads; nothing computed.
+// What the tile phase of the dissect kernels could reach on a batch's
+// layout (IMIX: one or two lines every 5 - 12 lines).
+template <bool NT>
+__global__ __launch_bounds__(256) void k_windows(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc,
+						 uint32_t n, uint32_t *sink)
+{
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t stride = gridDim.x * blockDim.x;
+	v4u acc = { 0, 0, 0, 0 };
+	for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
+		const uint64_t d = base + lane < n ? desc[base + lane] : 0;
+		const uint64_t a = (uint64_t)(uintptr_t)frames + ((d & ((1ull << 40) - 1)) & ~15ull);
+#pragma unroll
+		for (int r = 0; r < 4; r++) {
+			const int q = r * 16 + (int)(lane >> 2);
+			const uint64_t aq = (uint64_t)__shfl((uint32_t)a, q, 64) | (uint64_t)__shfl((uint32_t)(a >> 32), q, 64) << 32;
+			acc ^= ld<NT>((const v4u *)(uintptr_t)(aq + 16 * (lane & 3)));
+		}
+	}
+	if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9E3779B9u)
+		sink[0] = acc.x;
+}
+
+extern "C" int nsd_bw_windows(const void *frames, const void *desc, uint32_t n, int blocks_per_cu, int nontemporal,
+			      void *stream, uint32_t *sink)
+{
+	int dev = 0, cus = 0;
+	if (hipGetDevice(&dev) != hipSuccess ||
+	    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+		return -1;
+	const dim3 grid((unsigned)(cus * (blocks_per_cu > 0 ? blocks_per_cu : 4)));
+	if (nontemporal)
+		hipLaunchKernelGGL(k_windows<true>, grid, dim3(256), 0, (hipStream_t)stream, (const uint8_t *)frames,
+				   (const uint64_t *)desc, n, sink);
+	else
+		hipLaunchKernelGGL(k_windows<false>, grid, dim3(256), 0, (hipStream_t)stream, (const uint8_t *)frames,
+				   (const uint64_t *)desc, n, sink);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
