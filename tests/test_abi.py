@@ -52,6 +52,19 @@ def test_device_path_fails_loudly_without_gpu():
         nsd.entry_batch(frames, desc)
 
 
+def test_replay_fails_loudly_without_gpu(tmp_path):
+    """`--in` through the library needs the device walk: without a GPU the
+    replay reports an error (no CPU fallback), the pcap reader alone works."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    path = str(tmp_path / "x.pcap")
+    T.write_pcap(path, [b"\x00" * 64] * 3)
+    assert len(nsd.pcap_frame_hdrs(path)[1]) == 3
+    with pytest.raises(nsd.NsdError):
+        nsd.replay_pcap(path)
+
+
 def test_format_rejects_inconsistent_record():
     frames, desc = T.make_batch(T.SYN_UDP64, 4)
     rec, ext, _, _ = T.oracle_records(frames, desc)
