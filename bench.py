@@ -447,15 +447,16 @@ def ref_harness_rate(cfg, key, n=1 << 17, frames=True):
         T.synth().nsd_synth_pcap(cfg, T.SEED, 0, n, path.encode())
         t0 = time.perf_counter()
         r = subprocess.run([exe] + (["-f"] if frames else []) +
-                           ["-m", str(T.PRINT_NORM), "-w", "65535", "-i", os.path.join(d, "idx"), path],
+                           ["-m", str(T.PRINT_NORM), "-w", "0", "-i", os.path.join(d, "idx"), path],
                            stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
         dt = time.perf_counter() - t0
     if r.returncode != 0:
-        return None
+        return {"error": f"nsref rc={r.returncode}: {r.stderr.decode(errors='replace')[-200:]}"}
     return {"value": round(n / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "reference",
             "sample": f"{key}: {n} records, `nsref{' -f' if frames else ''}` "
                       f"({'frame header line (if_indextoname per packet, as the reference) + ' if frames else ''}"
-                      f"dissector text, unwrapped) to /dev/null in {dt:.2f} s, process start included"}
+                      f"dissector text, tprintf's 80-column wrap) to /dev/null in {dt:.2f} s, process start "
+                      f"included"}
 
 
 def cpu_baseline(key, seconds):
