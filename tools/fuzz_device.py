@@ -2,7 +2,7 @@
 several seeds, modes and alignments, both record forms (16-byte records
 through the host batch entry, compact records through the device-resident
 entry); prints mismatch counts.  GPU box tool:
-  python tools/fuzz_device.py [n] [seeds]"""
+  python tools/fuzz_device.py [n] [seeds] [split|fused]"""
 import os
 import sys
 
@@ -18,6 +18,8 @@ from test_device_parity import _check_compact, assert_same_records  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 200000
 seeds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+if len(sys.argv) > 3:   # split / fused (default: the adaptive choice)
+    nsd.set_schedule({"split": nsd.SCHED_SPLIT, "fused": nsd.SCHED_FUSED}[sys.argv[3]])
 fails = 0
 for seed in range(seeds):
     for mode, align in ((T.PRINT_NORM, 16), (T.PRINT_LESS, 16), (T.PRINT_NORM, 2)):
