@@ -77,12 +77,28 @@ struct Out {
 		w++;
 		return *this;
 	}
-	// %u
+	// %u (two digits per step)
 	Out &u(uint64_t v)
 	{
+		static const char d2[201] = "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+					    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+					    "8081828384858687888990919293949596979899";
+		if (v < 10)
+			return c((char)('0' + v));
 		char b[24];
 		int i = 24;
-		do { b[--i] = (char)('0' + v % 10); v /= 10; } while (v);
+		while (v >= 100) {
+			const uint32_t r = (uint32_t)(v % 100);
+			v /= 100;
+			b[--i] = d2[2 * r + 1];
+			b[--i] = d2[2 * r];
+		}
+		if (v >= 10) {
+			b[--i] = d2[2 * v + 1];
+			b[--i] = d2[2 * v];
+		} else {
+			b[--i] = (char)('0' + v);
+		}
 		return put(b + i, (size_t)(24 - i));
 	}
 	// %d / %zd
