@@ -957,12 +957,19 @@ static void dump_ascii(Out &o, const Frame &f, uint32_t from, uint32_t len)
 	if (!len)
 		return;
 	o << " [ Chr ";
+	const bool inside = (uint64_t)from + len <= f.caplen;   // (bytes past caplen read as zero)
 	for (uint32_t i0 = 0; i0 < len; i0 += 1024) {
 		const uint32_t m = len - i0 < 1024 ? len - i0 : 1024;
 		char *w = o.room(m);
-		for (uint32_t i = 0; i < m; i++) {
-			const uint8_t c = f.b(from + i0 + i);
-			w[i] = (c >= 0x20 && c < 0x7f) ? (char)c : '.';
+		if (inside) {
+			const uint8_t *q = f.p + from + i0;
+			for (uint32_t i = 0; i < m; i++)
+				w[i] = (q[i] >= 0x20 && q[i] < 0x7f) ? (char)q[i] : '.';
+		} else {
+			for (uint32_t i = 0; i < m; i++) {
+				const uint8_t c = f.b(from + i0 + i);
+				w[i] = (c >= 0x20 && c < 0x7f) ? (char)c : '.';
+			}
 		}
 		o.w += m;
 	}
@@ -975,11 +982,12 @@ static void dump_hex(Out &o, const Frame &f, uint32_t from, uint32_t len)
 	if (!len)
 		return;
 	o << " [ Hex ";
+	const bool inside = (uint64_t)from + len <= f.caplen;   // (bytes past caplen read as zero)
 	for (uint32_t i0 = 0; i0 < len; i0 += 512) {
 		const uint32_t m = len - i0 < 512 ? len - i0 : 512;
 		char *w = o.room(3 * (size_t)m);
 		for (uint32_t i = 0; i < m; i++) {
-			const uint8_t c = f.b(from + i0 + i);
+			const uint8_t c = inside ? f.p[from + i0 + i] : f.b(from + i0 + i);
 			w[3 * i] = ' ';
 			w[3 * i + 1] = hx[c >> 4];
 			w[3 * i + 2] = hx[c & 15];
