@@ -59,14 +59,24 @@ struct Out {
 			flush();
 		return w;
 	}
-	Out &put(const char *t, size_t n)
+	// literal-sized appends inline to a few stores; the rare flush / long
+	// append is out of line
+	__attribute__((always_inline)) Out &put(const char *t, size_t n)
 	{
+		if (__builtin_expect((size_t)(buf + sizeof(buf) - w) < n, 0))
+			return put_slow(t, n);
+		memcpy(w, t, n);
+		w += n;
+		return *this;
+	}
+	__attribute__((noinline)) Out &put_slow(const char *t, size_t n)
+	{
+		flush();
 		if (n > sizeof(buf) / 2) {
-			flush();
 			s.append(t, n);
 			return *this;
 		}
-		memcpy(room(n), t, n);
+		memcpy(w, t, n);
 		w += n;
 		return *this;
 	}
@@ -77,29 +87,38 @@ struct Out {
 		w++;
 		return *this;
 	}
-	// %u (two digits per step)
+	// %u (two digits per step, written in place)
 	Out &u(uint64_t v)
 	{
 		static const char d2[201] = "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
 					    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
 					    "8081828384858687888990919293949596979899";
-		if (v < 10)
-			return c((char)('0' + v));
-		char b[24];
-		int i = 24;
+		static const uint64_t p10[20] = { 1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull,
+			10000000ull, 100000000ull, 1000000000ull, 10000000000ull, 100000000000ull, 1000000000000ull,
+			10000000000000ull, 100000000000000ull, 1000000000000000ull, 10000000000000000ull,
+			100000000000000000ull, 1000000000000000000ull, 10000000000000000000ull };
+		char *p = room(20);
+		if (v < 10) {
+			*p = (char)('0' + v);
+			w = p + 1;
+			return *this;
+		}
+		// digits = floor(log10 v) + 1 from the bit length
+		int n = ((64 - __builtin_clzll(v)) * 1233) >> 12;
+		n += v >= p10[n];
+		char *e = p + n;
+		w = e;
 		while (v >= 100) {
 			const uint32_t r = (uint32_t)(v % 100);
 			v /= 100;
-			b[--i] = d2[2 * r + 1];
-			b[--i] = d2[2 * r];
+			e -= 2;
+			memcpy(e, d2 + 2 * r, 2);
 		}
-		if (v >= 10) {
-			b[--i] = d2[2 * v + 1];
-			b[--i] = d2[2 * v];
-		} else {
-			b[--i] = (char)('0' + v);
-		}
-		return put(b + i, (size_t)(24 - i));
+		if (v >= 10)
+			memcpy(e - 2, d2 + 2 * v, 2);
+		else
+			e[-1] = (char)('0' + v);
+		return *this;
 	}
 	// %d / %zd
 	Out &d(int64_t v)
@@ -120,11 +139,15 @@ struct Out {
 	Out &xn(uint64_t v, int n)
 	{
 		static const char hx[] = "0123456789abcdef";
-		char b[16];
-		int i = 16;
-		do { b[--i] = hx[v & 15]; v >>= 4; } while (v);
-		while (16 - i < n) b[--i] = '0';
-		return put(b + i, (size_t)(16 - i));
+		const int bits = v ? 64 - __builtin_clzll(v) : 1;
+		int k = (bits + 3) >> 2;
+		if (k < n)
+			k = n;
+		char *p = room(16 + (size_t)(n > 16 ? n - 16 : 0));
+		w = p + k;
+		for (int i = k - 1; i >= 0; i--, v >>= 4)
+			p[i] = hx[v & 15];
+		return *this;
 	}
 };
 
