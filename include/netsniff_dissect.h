@@ -559,6 +559,13 @@ long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_
 long nsd_pcap_read_batch_fh(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
 			    nsd_sll_t *sll, nsd_frame_hdr_t *fh, uint32_t max_n);
 void nsd_pcap_close(nsd_pcap *p);
+/* nsd_pcap_index: a mapped pcap file's record walk as the replay reader
+ * builds it (windows of `window` bytes, 0 = the replay's; each cut into
+ * `chunks` walked in parallel from guessed record starts and spliced onto
+ * the exact walk): the first max_n records' header offsets and caplens.
+ * Returns the records found (read_batch's end rule) or NSD_ERR_ARG. */
+long nsd_pcap_index(const char *path, uint64_t window, int chunks, uint64_t *off, uint32_t *caplen,
+		    size_t max_n);
 long nsd_replay_pcap(const char *path, int mode, const struct nsd_bpf_prog *filter, int out_fd,
 		     int cols, uint64_t *counters, int threads);
 /* nsd_replay_pcap plus `--out f.pcap` (read_pcap netsniff-ng.c:636, 693-697,

@@ -80,7 +80,7 @@ struct Out {
 		w += n;
 		return *this;
 	}
-	Out &operator<<(const char *t) { return put(t, strlen(t)); }
+	__attribute__((always_inline)) Out &operator<<(const char *t) { return put(t, strlen(t)); }
 	Out &c(char ch)
 	{
 		*room(1) = ch;
@@ -195,11 +195,34 @@ static bool lay3_has(uint32_t k)
 	return false;
 }
 
-static void ntop4(const Frame &f, uint64_t off, char *buf)
+// decimal text of each octet value, its length in the 4th byte
+struct OctetText {
+	char t[256][4];
+	constexpr OctetText() : t()
+	{
+		for (int v = 0; v < 256; v++) {
+			int n = 0;
+			if (v >= 100) t[v][n++] = (char)('0' + v / 100);
+			if (v >= 10) t[v][n++] = (char)('0' + v / 10 % 10);
+			t[v][n++] = (char)('0' + v % 10);
+			t[v][3] = (char)n;
+		}
+	}
+};
+static constexpr OctetText k_octet{};
+
+// the IPv4 address at off as inet_ntop prints it, straight into the sink
+static void quad(Out &o, const Frame &f, uint64_t off)
 {
-	uint8_t a[4];
-	for (int i = 0; i < 4; i++) a[i] = f.b(off + i);
-	ntop4_to(a, buf);   // inet_ntop's text (nsd_ntop.h)
+	char *w = o.room(16);   // 4 x 4-byte stores, the last may run 1 past the text
+	for (int i = 0; i < 4; i++) {
+		const char *t = k_octet.t[f.b(off + i)];
+		memcpy(w, t, 4);
+		w += (uint8_t)t[3];
+		if (i < 3)
+			*w++ = '.';
+	}
+	o.w = w;
 }
 
 static void ntop6(const Frame &f, uint64_t off, char *buf)
@@ -335,14 +358,15 @@ static Done r_ipv4(Out &o, const Frame &f, const Layer &L, int mode, uint16_t ip
 	const uint8_t ihl = f.b(ip) & 0xF;
 	const uint16_t tot_len = f.be16(ip + 2);
 	const uint8_t proto = f.b(ip + 9);
-	char s[INET_ADDRSTRLEN], dd[INET_ADDRSTRLEN];
-	ntop4(f, ip + 12, s);
-	ntop4(f, ip + 16, dd);
 	uint32_t data = ip + 20, tail = L.tail;
 	const uint32_t opts_len = (ihl > 5 ? ihl : 5) * 4u - 20u;
 
 	if (mode != PRINT_NORM) {
-		o << " " << s << "/" << dd << " Len ";
+		o << " ";
+		quad(o, f, ip + 12);
+		o << "/";
+		quad(o, f, ip + 16);
+		o << " Len ";
 		o.u(tot_len);
 		if (opts_len <= tail - data)
 			data += opts_len;
@@ -362,7 +386,11 @@ static Done r_ipv4(Out &o, const Frame &f, const Layer &L, int mode, uint16_t ip
 		}
 	}
 	const uint16_t frag = f.be16(ip + 6);
-	o << " [ IPv4 Addr (" << s << " => " << dd << "), Proto (";
+	o << " [ IPv4 Addr (";
+	quad(o, f, ip + 12);
+	o << " => ";
+	quad(o, f, ip + 16);
+	o << "), Proto (";
 	o.u(proto) << "), TTL (";
 	o.u(f.b(ip + 8)) << "), TOS (";
 	o.u(f.b(ip + 1)) << "), Ver (";

@@ -35,9 +35,7 @@ static void tputs_safe(Out &o, const Frame &f, uint64_t off, uint64_t len)
 
 static void ip4(Out &o, const Frame &f, uint64_t off)
 {
-	uint8_t a[4];
-	for (int i = 0; i < 4; i++) a[i] = f.b(off + i);
-	o.w = ntop4_to(a, o.room(INET_ADDRSTRLEN));   // 15 chars + NUL, NUL not kept
+	quad(o, f, off);
 }
 
 // ---- ARP (proto_arp.c:52-196) -------------------------------------------------

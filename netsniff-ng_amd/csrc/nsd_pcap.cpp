@@ -42,6 +42,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -89,6 +90,13 @@ struct nsd_pcap {
 	std::vector<uint8_t> buf;
 	const uint8_t *map = nullptr;
 	size_t pos = 0, len = 0;
+	// a mapped file's record index, one window at a time (RecIndex below):
+	// the records' header offsets and caplens, ix_i the next one; ix_end =
+	// the walk ended inside the indexed window (no records past the last)
+	std::vector<uint64_t> ix_off;
+	std::vector<uint32_t> ix_cap;
+	size_t ix_i = 0;
+	bool ix_end = false;
 
 	const uint8_t *data() const { return map ? map : buf.data(); }
 	bool fill(size_t need)
@@ -350,43 +358,57 @@ static long scan_batch(nsd_pcap *p, size_t cap, nsd_desc_t *desc, uint64_t *src,
 	size_t off = 0;
 	uint32_t n = 0;
 	const uint32_t hs = p->hdrsize;
-	while (n < max_n && !p->eof) {
-		if (p->len - p->pos < hs) {
-			p->eof = true;
-			break;
+	*end = 0;
+	if (p->eof)
+		return 0;
+	// (a record read past the index by read_one)
+	while (p->ix_i < p->ix_off.size() && p->ix_off[p->ix_i] < p->pos)
+		p->ix_i++;
+	// (locals: the stores to desc / src could alias p's fields)
+	const uint64_t *const ixo = p->ix_off.data();
+	const uint32_t *const ixc = p->ix_cap.data();
+	const size_t ixn = p->ix_off.size();
+	size_t i = p->ix_i;
+	long rc = 0;
+	while (n < max_n) {
+		if (i == ixn) {
+			if (p->ix_end)
+				p->eof = true;
+			break;   // (the caller builds the next window)
 		}
-		uint32_t cl;
-		memcpy(&cl, p->map + p->pos + 8, 4);
-		if (p->swapped)
-			cl = bswap32(cl);
-		const uint32_t caplen = cl - p->ll_extra;
-		if (caplen == 0 || caplen > REPLAY_BUF) {
-			p->eof = true;
-			break;
-		}
+		const uint32_t caplen = ixc[i];
 		if (caplen > NSD_MAX_CAPLEN) {
 			if (n == 0)
-				return NSD_ERR_CAPLEN;
+				rc = NSD_ERR_CAPLEN;
 			break;
 		}
 		const size_t at = (off + 15) & ~(size_t)15;
 		if (at + caplen + NSD_FRAME_PAD > cap) {
 			if (n == 0)
-				return NSD_ERR_ARG;
+				rc = NSD_ERR_ARG;
 			break;
 		}
-		if (p->len - p->pos < (size_t)hs + caplen) {
-			p->eof = true;
-			break;
-		}
-		src[n] = p->pos;
+		src[n] = ixo[i];
 		desc[n] = NSD_DESC(at, caplen);
-		p->pos += hs + caplen;
+		i++;
 		off = at + caplen;
 		n++;
 	}
+	if (n) {
+		p->pos = ixo[i - 1] + hs + ixc[i - 1];
+		p->ix_i = i;
+	}
 	*end = off;
-	return n;
+	return rc ? rc : n;
+}
+
+// the index window under p->pos is used up (and the walk goes on)
+static bool ix_need(const nsd_pcap *p)
+{
+	size_t i = p->ix_i;
+	while (i < p->ix_off.size() && p->ix_off[i] < p->pos)
+		i++;
+	return i == p->ix_off.size() && !p->ix_end && !p->eof;
 }
 
 static void fill_range(const nsd_pcap *p, uint8_t *frames, const nsd_desc_t *desc, const uint64_t *src,
@@ -400,6 +422,208 @@ static void fill_range(const nsd_pcap *p, uint8_t *frames, const nsd_desc_t *des
 			memcpy(rhdr + 32 * (size_t)k, h, hs);
 		record_meta(p, h, sll + k, fh + k);
 	}
+}
+
+// ---- a mapped file's record index, built in parallel ----------------------
+// The record walk (each header's caplen gives the next header) is one
+// dependent load per record: walked by one thread it bounds the replay's
+// reader (a 64-byte frame every 80 bytes touches every line of the file).
+// A window of the file is cut into chunks; chunk 0 is walked from the exact
+// record start, every later chunk from a guess (the first offset from which
+// several headers in a row look like records); the exact walk then runs
+// through the chunks' results: the exact offset X where it enters chunk c is
+// looked up among the offsets chunk c visited, and from there chunk c's walk
+// IS the exact walk (a walk is determined by its start).  A chunk whose walk
+// never met X (a wrong guess that did not fall into step) is walked again
+// from X.  The end rule is read_batch's: a header past the file end, caplen 0
+// or > the 1 MiB replay buffer, or a body past the file end ends the walk.
+struct IxChunk {
+	std::vector<uint64_t> off;
+	std::vector<uint32_t> cap;
+	size_t next = 0;     // where the walk stopped (its last record's end)
+	bool ended = false;  // stopped by the end rule, not at the chunk's end
+};
+
+// caplen of the header at pos, or 0 when the end rule stops there
+static uint32_t rec_caplen(const nsd_pcap *p, size_t pos)
+{
+	const uint32_t hs = p->hdrsize;
+	if (p->len - pos < hs)
+		return 0;
+	uint32_t cl;
+	memcpy(&cl, p->map + pos + 8, 4);
+	if (p->swapped)
+		cl = bswap32(cl);
+	const uint32_t caplen = cl - p->ll_extra;
+	if (caplen == 0 || caplen > REPLAY_BUF || p->len - pos - hs < caplen)
+		return 0;
+	return caplen;
+}
+
+// the walk from pos while pos < stop_at, appended to c
+static void ix_walk(const nsd_pcap *p, size_t pos, size_t stop_at, IxChunk &c)
+{
+	const uint32_t hs = p->hdrsize;
+	c.ended = false;
+	while (pos < stop_at) {
+		if (p->len - pos > 4096 + 64)
+			__builtin_prefetch(p->map + pos + 4096);
+		const uint32_t caplen = rec_caplen(p, pos);
+		if (!caplen) {
+			c.ended = true;
+			break;
+		}
+		c.off.push_back(pos);
+		c.cap.push_back(caplen);
+		pos += hs + caplen;
+	}
+	c.next = pos;
+}
+
+// a record start for a walk from inside [lo, hi): the first offset whose next
+// 8 headers pass the end rule with a plausible fraction-of-second field (or
+// reach the file end exactly); hi when there is none
+static size_t ix_guess(const nsd_pcap *p, size_t lo, size_t hi)
+{
+	const uint32_t hs = p->hdrsize;
+	const uint32_t frac_max = p->nsec ? 1000000000u : 1000000u;
+	for (size_t o = lo; o < hi; o++) {
+		size_t q = o;
+		int k = 0;
+		for (; k < 8; k++) {
+			if (q == p->len)
+				break;
+			const uint32_t caplen = rec_caplen(p, q);
+			if (!caplen)
+				break;
+			uint32_t frac;
+			memcpy(&frac, p->map + q + 4, 4);
+			if ((p->swapped ? bswap32(frac) : frac) >= frac_max)
+				break;
+			q += hs + caplen;
+		}
+		if (k == 8 || (k > 0 && q == p->len))
+			return o;
+	}
+	return hi;
+}
+
+// chunk c of the window [b[0], b[nc]): walked from its guess to b[c + 1]
+static void ix_chunk(const nsd_pcap *p, const std::vector<size_t> &b, int c, IxChunk &out)
+{
+	out.off.clear();
+	out.cap.clear();
+	const size_t from = c == 0 ? b[0] : ix_guess(p, b[c], b[c + 1]);
+	out.next = from;
+	out.ended = false;
+	if (from < b[c + 1])
+		ix_walk(p, from, b[c + 1], out);
+}
+
+// the window's chunk bounds from the exact record start `start`
+static std::vector<size_t> ix_bounds(const nsd_pcap *p, size_t start, size_t window, int nc)
+{
+	const size_t end = p->len - start < window ? p->len : start + window;
+	std::vector<size_t> b(nc + 1);
+	for (int c = 0; c <= nc; c++)
+		b[c] = start + (end - start) * (size_t)c / (size_t)nc;
+	b[nc] = end;
+	return b;
+}
+
+// the exact walk through the chunks' results into p's index
+static void ix_splice(nsd_pcap *p, const std::vector<size_t> &b, std::vector<IxChunk> &ch)
+{
+	const int nc = (int)ch.size();
+	p->ix_off.clear();
+	p->ix_cap.clear();
+	p->ix_i = 0;
+	p->ix_end = false;
+	size_t x = b[0];
+	for (int c = 0; c < nc; c++) {
+		if (x >= b[c + 1])
+			continue;   // a record across the whole chunk
+		IxChunk &k = ch[c];
+		const auto it = std::lower_bound(k.off.begin(), k.off.end(), (uint64_t)x);
+		if (!(it != k.off.end() && *it == x) && !(k.ended && k.next == x)) {
+			// the guess never fell into step: walk the chunk again from x
+			k.off.clear();
+			k.cap.clear();
+			ix_walk(p, x, b[c + 1], k);
+			p->ix_off.insert(p->ix_off.end(), k.off.begin(), k.off.end());
+			p->ix_cap.insert(p->ix_cap.end(), k.cap.begin(), k.cap.end());
+		} else {
+			const size_t i = (size_t)(it - k.off.begin());
+			p->ix_off.insert(p->ix_off.end(), k.off.begin() + (long)i, k.off.end());
+			p->ix_cap.insert(p->ix_cap.end(), k.cap.begin() + (long)i, k.cap.end());
+		}
+		x = k.next;
+		if (k.ended) {
+			p->ix_end = true;
+			return;
+		}
+	}
+	// the window reached the file end: the walk ends there
+	if (b[nc] == p->len && x >= p->len)
+		p->ix_end = true;
+}
+
+// the index window from p->pos, chunks run by run(nc, fn) (fn(c) for each
+// chunk c, in any order and on any threads)
+template <class Run>
+static void ix_build(nsd_pcap *p, size_t window, int nc, std::vector<IxChunk> &ch, Run run)
+{
+	const std::vector<size_t> b = ix_bounds(p, p->pos, window, nc);
+	if ((int)ch.size() != nc)
+		ch.resize(nc);
+	run(nc, std::function<void(int)>([&](int c) { ix_chunk(p, b, c, ch[c]); }));
+	ix_splice(p, b, ch);
+}
+
+// the index window (bytes of file per build; NSD_PCAP_IX_WINDOW overrides,
+// for tests)
+static size_t ix_window()
+{
+	const char *e = getenv("NSD_PCAP_IX_WINDOW");
+	const long long v = e ? atoll(e) : 0;
+	return v > 0 ? (size_t)v : (size_t)16 << 20;
+}
+
+// The record index of a mapped file (the replay reader's, windows of
+// `window` bytes, 0 = the replay's, cut into `chunks` walked from guesses and
+// spliced): the first max_n records' header offsets and caplens into off /
+// caplen.  Returns the records the walk finds (read_batch's end rule), or
+// NSD_ERR_ARG (not a pcap file, or not a regular file).
+extern "C" long nsd_pcap_index(const char *path, uint64_t window, int chunks, uint64_t *off, uint32_t *caplen,
+			       size_t max_n)
+{
+	nsd_pcap *p = nsd_pcap_open(path);
+	if (!p)
+		return NSD_ERR_ARG;
+	if (!p->map || (max_n && (!off || !caplen))) {
+		nsd_pcap_close(p);
+		return NSD_ERR_ARG;
+	}
+	std::vector<IxChunk> ch;
+	size_t n = 0;
+	while (ix_need(p)) {
+		// (chunks run last to first: the splice does not depend on the order)
+		ix_build(p, window ? (size_t)window : ix_window(), chunks < 1 ? 1 : chunks, ch,
+			 [](int nc, const std::function<void(int)> &fn) {
+				 for (int c = nc - 1; c >= 0; c--)
+					 fn(c);
+			 });
+		for (size_t i = 0; i < p->ix_off.size(); i++, n++)
+			if (n < max_n) {
+				off[n] = p->ix_off[i];
+				caplen[n] = p->ix_cap[i];
+			}
+		if (!p->ix_off.empty())
+			p->pos = p->ix_off.back() + p->hdrsize + p->ix_cap.back();
+		p->ix_i = p->ix_off.size();
+	}
+	nsd_pcap_close(p);
+	return (long)n;
 }
 
 // The next record whatever its length (<= the 1 MiB replay buffer), for the
@@ -493,7 +717,7 @@ namespace {
 constexpr uint32_t BATCH = 1u << 16;
 constexpr size_t FRAME_BYTES = 32ull << 20;
 constexpr int DEPTH = 3;           // batches on the device
-constexpr int NSLOT = DEPTH + 3;   // + being rendered, rendered, being written
+constexpr int NSLOT = DEPTH + 4;   // + being copied, being rendered, rendered, being written
 // the side words and room for a quarter of a batch to take a deep (> 12
 // layer) entry; a chain the pool cannot hold is rendered per packet
 constexpr uint32_t EXT_WORDS = BATCH + BATCH / 4 * NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS);
@@ -659,7 +883,7 @@ std::vector<int> pool_cpus()
 // the device waits, the formatter jobs (summed over the pool), the writer,
 // and the reader's waits for a free slot.
 struct ReplayStats {
-	std::atomic<uint64_t> read{ 0 }, dev{ 0 }, fmt{ 0 }, write{ 0 }, slot{ 0 }, jobs{ 0 };
+	std::atomic<uint64_t> read{ 0 }, scan{ 0 }, ix{ 0 }, dev{ 0 }, fmt{ 0 }, write{ 0 }, slot{ 0 }, jobs{ 0 };
 	static uint64_t now()
 	{
 		return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -746,6 +970,9 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		std::vector<TextPart> *part = nullptr;   // res.part[slot]
 		long prc = NSD_OK;         // first render error
 	};
+	// render jobs per formatter thread and batch (fill jobs wait for the
+	// render job in hand)
+	const int split = getenv("NSD_REPLAY_SPLIT") ? std::max(1, atoi(getenv("NSD_REPLAY_SPLIT"))) : 1;
 	std::vector<Slot> b(NSLOT);
 	std::vector<uint32_t> verdicts(filter ? (size_t)NSLOT * BATCH : 0);
 	std::vector<uint8_t> rhdrs(pcap_fd >= 0 ? (size_t)NSLOT * BATCH * 32 : 0);
@@ -761,8 +988,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		x.verdict = filter ? &verdicts[(size_t)k * BATCH] : nullptr;
 		x.rhdr = pcap_fd >= 0 ? &rhdrs[(size_t)k * BATCH * 32] : nullptr;
 		x.part = &res.part[k];
-		if (x.part->size() < (size_t)threads)
-			x.part->resize(threads);
+		if (x.part->size() < (size_t)(threads * split))
+			x.part->resize((size_t)(threads * split));
 	}
 
 	std::mutex mu;
@@ -770,12 +997,13 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	ReplayStats st;
 	const bool stats = getenv("NSD_REPLAY_STATS") != nullptr;
 	const uint64_t t_start = ReplayStats::now();
-	// (slot, part, parts): render jobs, and copy jobs (parts > 0) of a mapped
-	// file's batch, which go first
+	// (slot, part, parts): render jobs, and the jobs of a mapped file's
+	// reader (copies of a batch, parts > 0; record index chunks, slot -1),
+	// which the pool takes first, in the order given
 	struct Job {
 		int slot, part, parts;
 	};
-	std::deque<Job> jobs;
+	std::deque<Job> jobs, fills;
 	std::vector<int> free_slots;
 	for (int k = NSLOT - 1; k >= 0; k--)
 		free_slots.push_back(k);
@@ -886,31 +1114,78 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		const uint32_t lo = (uint32_t)((uint64_t)x.n * q / parts), hi = (uint32_t)((uint64_t)x.n * (q + 1) / parts);
 		fill_range(p, x.frames, x.desc, x.src, lo, hi, x.sll, x.fh, x.rhdr);
 	};
-	// the copy of a scanned batch (x.n records in slot k): parts 1.. on the
-	// pool, ahead of its render jobs, part 0 and whatever is left here
-	auto fill_batch = [&](Slot &x, int k) {
+	// the copy of a scanned batch (x.n records in slot k) goes to the pool
+	// while the reader scans the next batch; wait_fill joins it (the reader
+	// takes the batch's parts still queued)
+	auto start_fill = [&](Slot &x, int k) {
 		const int parts = x.n < 4096 ? 1 : (int)std::min<uint32_t>((uint32_t)threads + 1, x.n / 2048);
-		std::unique_lock<std::mutex> lk(mu);
-		x.fill_left = parts - 1;
-		for (int q = parts - 1; q >= 1; q--)
-			jobs.push_front({ k, q, parts });
-		if (parts > 1)
-			cv_job.notify_all();
+		std::lock_guard<std::mutex> g(mu);
+		x.fill_left = parts;
+		for (int q = 0; q < parts; q++)
+			fills.push_back({ k, q, parts });
+		cv_job.notify_all();
+	};
+	// the record index's chunk jobs (slot -1) of the window being built
+	std::function<void(int)> ix_fn;
+	int ix_left = 0;
+	std::vector<IxChunk> ix_chunks;
+	// the front copy job, taken with mu held (returns with it held)
+	auto run_fill = [&](std::unique_lock<std::mutex> &lk) {
+		const Job j = fills.front();
+		fills.pop_front();
 		lk.unlock();
-		fill_part(x, 0, parts);
+		if (j.slot < 0)
+			ix_fn(j.part);
+		else
+			fill_part(b[j.slot], j.part, j.parts);
 		lk.lock();
+		if (j.slot < 0 ? --ix_left == 0 : --b[j.slot].fill_left == 0)
+			cv_fill.notify_all();
+	};
+	auto wait_fill = [&](Slot &x) {
+		std::unique_lock<std::mutex> lk(mu);
 		while (x.fill_left > 0) {
-			if (!jobs.empty() && jobs.front().parts > 0 && jobs.front().slot == k) {
-				const Job j = jobs.front();
-				jobs.pop_front();
-				lk.unlock();
-				fill_part(x, j.part, j.parts);
-				lk.lock();
-				x.fill_left--;
-				continue;
-			}
-			cv_fill.wait(lk);
+			if (!fills.empty())
+				run_fill(lk);   // (in file order: this batch's or an earlier one's)
+			else
+				cv_fill.wait(lk);
 		}
+	};
+	// a mapped file's index windows: the chunks of the window after the one
+	// the reader scans run on the pool meanwhile (a window's start is the end
+	// of the one before, known once that one is spliced)
+	std::vector<size_t> ix_b;
+	bool ix_flight = false;
+	auto ix_launch = [&](size_t start) {
+		const int nc = threads + 1;
+		ix_b = ix_bounds(p, start, ix_window(), nc);
+		if ((int)ix_chunks.size() != nc)
+			ix_chunks.resize(nc);
+		std::lock_guard<std::mutex> g(mu);
+		ix_fn = [&](int c) { ix_chunk(p, ix_b, c, ix_chunks[c]); };
+		ix_left = nc;
+		for (int c = 0; c < nc; c++)
+			fills.push_back({ -1, c, nc });
+		ix_flight = true;
+		cv_job.notify_all();
+	};
+	auto ix_join = [&]() {
+		std::unique_lock<std::mutex> lk(mu);
+		while (ix_left > 0) {
+			if (!fills.empty())
+				run_fill(lk);
+			else
+				cv_fill.wait(lk);
+		}
+		ix_flight = false;
+	};
+	auto build_index = [&]() {
+		if (!ix_flight)
+			ix_launch(p->pos);
+		ix_join();
+		ix_splice(p, ix_b, ix_chunks);
+		if (!p->ix_end)
+			ix_launch(p->ix_off.empty() ? ix_b[0] : p->ix_off.back() + p->hdrsize + p->ix_cap.back());
 	};
 	std::vector<std::thread> pool;
 	const std::vector<int> cpus = pool_cpus();
@@ -927,19 +1202,16 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			}
 			std::unique_lock<std::mutex> lk(mu);
 			for (;;) {
-				cv_job.wait(lk, [&] { return stop || !jobs.empty(); });
-				if (jobs.empty())
+				cv_job.wait(lk, [&] { return stop || !jobs.empty() || !fills.empty(); });
+				if (jobs.empty() && fills.empty())
 					return;
+				if (!fills.empty()) {
+					run_fill(lk);
+					continue;
+				}
 				const Job j = jobs.front();
 				jobs.pop_front();
 				lk.unlock();
-				if (j.parts > 0) {
-					fill_part(b[j.slot], j.part, j.parts);
-					lk.lock();
-					if (--b[j.slot].fill_left == 0)
-						cv_fill.notify_all();
-					continue;
-				}
 				const uint64_t t0 = stats ? ReplayStats::now() : 0;
 				const long r = render(b[j.slot], j.part);
 				if (stats) {
@@ -1000,7 +1272,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			for (int c = 0; c < NSD_NCOUNTERS; c++)
 				counters[c] += x.cnt[c];
 		std::lock_guard<std::mutex> g(mu);
-		x.parts = x.n < 2048 ? 1 : threads;
+		x.parts = x.n < 2048 ? 1 : (int)std::min<uint32_t>((uint32_t)(threads * split), x.n / 1024);
 		x.left = x.parts;
 		x.prc = r;
 		x.seq = next_seq++;
@@ -1062,6 +1334,59 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		return r;
 	};
 
+	// slot k's n records read: filtered (bpf_run_filter per record before the
+	// dissector, netsniff-ng.c:723-725) and submitted to the device
+	auto give_back = [&](int slot) {
+		std::lock_guard<std::mutex> g(mu);
+		free_slots.push_back(slot);
+	};
+	auto submit_slot = [&](int k, long n) -> long {
+		Slot &x = b[k];
+		size_t used = 0;
+		for (long j = 0; j < n; j++) {
+			const size_t e = NSD_DESC_OFF(x.desc[j]) + NSD_DESC_CAPLEN(x.desc[j]);
+			used = e > used ? e : used;
+		}
+		if (filter) {
+			// bpf_run_filter per record before the dissector (netsniff-ng.c:723-725)
+			int r = nsd_bpf_filter_batch(filter, x.frames, used, x.desc, (uint32_t)n, x.verdict);
+			if (r != NSD_OK) {
+				give_back(k);
+				return r;
+			}
+			long m = 0;
+			for (long j = 0; j < n; j++)
+				if (x.verdict[j]) {
+					x.sll[m] = x.sll[j];
+					x.fh[m] = x.fh[j];
+					if (x.rhdr && m != j)
+						memcpy(x.rhdr + 32 * (size_t)m, x.rhdr + 32 * (size_t)j, 32);
+					x.desc[m++] = x.desc[j];
+				}
+			n = m;
+			if (n == 0) {
+				give_back(k);
+				return NSD_OK;
+			}
+		}
+		if ((int)on_device.size() == DEPTH)
+			complete_oldest();
+		x.n = (uint32_t)n;
+		x.count0 = counted + 1;
+		counted += x.n;
+		x.status = NSD_OK;
+		memset(x.cnt, 0, sizeof(x.cnt));
+		int r = nsd_pipe_submit_compact(pipe, x.frames, used, x.desc, has_ll ? x.sll : nullptr, x.n, x.rec, x.ext,
+						&x.ext_used, x.cnt, &x.status);
+		if (r != NSD_OK) {
+			give_back(k);
+			return r;
+		}
+		on_device.push_back(k);
+		return NSD_OK;
+	};
+	int pend = -1;     // a mapped file's batch whose copy is on the pool
+	long pend_n = 0;
 	while (rc == NSD_OK) {
 		int k;
 		{
@@ -1086,79 +1411,72 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			free_slots.pop_back();
 		}
 		Slot &x = b[k];
-		auto give_back = [&]() {
-			std::lock_guard<std::mutex> g(mu);
-			free_slots.push_back(k);
-		};
 		const uint64_t tr = stats ? ReplayStats::now() : 0;
 		long n;
 		if (p->map) {
 			size_t end = 0;
+			if (ix_need(p)) {
+				build_index();
+				if (stats)
+					st.ix += ReplayStats::now() - tr;
+			}
 			n = scan_batch(p, FRAME_BYTES, x.desc, x.src, BATCH, &end);
+			if (stats)
+				st.scan += ReplayStats::now() - tr;
 			if (n > 0) {
 				x.n = (uint32_t)n;
-				fill_batch(x, k);
 				memset(x.frames + end, 0, NSD_FRAME_PAD);
+				start_fill(x, k);
 			}
 		} else {
 			n = read_batch(p, x.frames, FRAME_BYTES, x.desc, x.sll, x.fh, BATCH, nullptr, nullptr, x.rhdr);
 		}
+		// the mapped batch before this one: its copy done, on to the device
+		// (file order)
+		if (pend >= 0) {
+			const int j = pend;
+			pend = -1;
+			wait_fill(b[j]);
+			const long r = submit_slot(j, pend_n);
+			if (r != NSD_OK) {
+				if (n > 0 && p->map)
+					wait_fill(x);
+				give_back(k);
+				rc = r;
+				break;
+			}
+		}
 		if (stats)
 			st.read += ReplayStats::now() - tr;
 		if (n == NSD_ERR_CAPLEN) {
-			give_back();
+			give_back(k);
 			rc = one_big();
 			continue;
 		}
 		if (n <= 0) {
-			give_back();
+			give_back(k);
 			if (n < 0)
 				rc = n;
 			break;
 		}
-		size_t used = 0;
-		for (long j = 0; j < n; j++) {
-			const size_t e = NSD_DESC_OFF(x.desc[j]) + NSD_DESC_CAPLEN(x.desc[j]);
-			used = e > used ? e : used;
+		if (p->map) {
+			pend = k;
+			pend_n = n;
+			continue;
 		}
-		if (filter) {
-			// bpf_run_filter per record before the dissector (netsniff-ng.c:723-725)
-			int r = nsd_bpf_filter_batch(filter, x.frames, used, x.desc, (uint32_t)n, x.verdict);
-			if (r != NSD_OK) {
-				give_back();
-				rc = r;
-				break;
-			}
-			long m = 0;
-			for (long j = 0; j < n; j++)
-				if (x.verdict[j]) {
-					x.sll[m] = x.sll[j];
-					x.fh[m] = x.fh[j];
-					if (x.rhdr && m != j)
-						memcpy(x.rhdr + 32 * (size_t)m, x.rhdr + 32 * (size_t)j, 32);
-					x.desc[m++] = x.desc[j];
-				}
-			n = m;
-			if (n == 0) {
-				give_back();
-				continue;
-			}
-		}
-		if ((int)on_device.size() == DEPTH)
-			complete_oldest();
-		x.n = (uint32_t)n;
-		x.count0 = counted + 1;
-		counted += x.n;
-		x.status = NSD_OK;
-		memset(x.cnt, 0, sizeof(x.cnt));
-		int r = nsd_pipe_submit_compact(pipe, x.frames, used, x.desc, has_ll ? x.sll : nullptr, x.n, x.rec, x.ext,
-						&x.ext_used, x.cnt, &x.status);
+		const long r = submit_slot(k, n);
 		if (r != NSD_OK) {
-			give_back();
 			rc = r;
 			break;
 		}
-		on_device.push_back(k);
+	}
+	if (ix_flight)
+		ix_join();   // (an index window no scan reached)
+	if (pend >= 0) {
+		// (left by an error: its copy drains before the slots go away)
+		wait_fill(b[pend]);
+		std::lock_guard<std::mutex> g(mu);
+		free_slots.push_back(pend);
 	}
 	{
 		const long r = flush_all();
@@ -1176,9 +1494,9 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	writer.join();
 	if (stats)
 		fprintf(stderr,
-			"nsd_replay: %ld records, %d threads, %.1f ms: read %.1f, device waits %.1f, slot waits %.1f, "
+			"nsd_replay: %ld records, %d threads, %.1f ms: read %.1f (scan %.1f, index %.1f), device waits %.1f, slot waits %.1f, "
 			"format %.1f (%llu jobs, %.1f per thread), write %.1f ms\n",
-			printed, threads, (ReplayStats::now() - t_start) / 1e6, st.read / 1e6, st.dev / 1e6, st.slot / 1e6,
+			printed, threads, (ReplayStats::now() - t_start) / 1e6, st.read / 1e6, st.scan / 1e6, st.ix / 1e6, st.dev / 1e6, st.slot / 1e6,
 			st.fmt / 1e6, (unsigned long long)st.jobs.load(), st.fmt / 1e6 / threads, st.write / 1e6);
 	// (an error leaves batches in the pipe: drop the cached set then)
 	if (&res == &own || rc != NSD_OK)

@@ -79,7 +79,7 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_dissect_device_compact", "nsd_format_batch_compact", "nsd_pipe_create_compact",
                "nsd_pipe_submit_compact", "nsd_format_range_compact", "nsd_set_schedule",
                "nsd_last_schedule", "nsd_format_frame_hdr", "nsd_format_range_compact_fh",
-               "nsd_pcap_read_batch_fh", "nsd_t3_block_desc_fh"]
+               "nsd_pcap_read_batch_fh", "nsd_t3_block_desc_fh", "nsd_pcap_index"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -215,6 +215,7 @@ def lib():
                  [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _int, _int, _vp, _vp, _vp, _sz, _vp, _vp]),
                 ("nsd_pcap_read_batch_fh", ctypes.c_long, [_vp, _vp, _sz, _vp, _vp, _vp, _u32]),
                 ("nsd_t3_block_desc_fh", ctypes.c_long, [_vp, _sz, _int, _int, _vp, _vp, _vp, _u32]),
+                ("nsd_pcap_index", ctypes.c_long, [ctypes.c_char_p, _u64, _int, _vp, _vp, _sz]),
                 ("nsd_last_schedule", _int, [])):
             if hasattr(L, name):
                 getattr(L, name).restype = res
@@ -684,6 +685,22 @@ def pcap_frame_hdrs(path, cap=64 << 20, max_n=1 << 16):
         return lt, pkts, fh, ll
     finally:
         L.nsd_pcap_close(h)
+
+
+def pcap_index(path, window=0, chunks=1):
+    """The replay reader's record index of a mapped pcap file
+    (nsd_pcap_index): (header offsets uint64, caplens uint32), windows of
+    `window` bytes (0: the replay's) cut into `chunks` walked from guesses."""
+    L = lib()
+    n = L.nsd_pcap_index(os.fsencode(path), window, chunks, None, None, 0)
+    if n < 0:
+        raise NsdError(f"nsd_pcap_index({path}) failed with status {n}")
+    off = np.zeros(max(n, 1), dtype=np.uint64)
+    cap = np.zeros(max(n, 1), dtype=np.uint32)
+    m = L.nsd_pcap_index(os.fsencode(path), window, chunks, off.ctypes.data, cap.ctypes.data, n)
+    if m != n:
+        raise NsdError(f"nsd_pcap_index({path}): {m} records, then {n}")
+    return off[:n], cap[:n]
 
 
 def format_frame_hdr(fh, pkt=b"", sll=None, linktype=LINKTYPE_EN10MB, mode=PRINT_NORM, count=1):

@@ -173,6 +173,84 @@ def test_reader_mapped_and_read_paths_agree(tmp_path, monkeypatch):
     assert got[1] == ref[1] and np.array_equal(got[2], ref[2])
 
 
+def _walk(path):
+    """The record walk one header at a time (read_batch's end rule): each
+    record's (header offset, caplen)."""
+    data = open(path, "rb").read()
+    magic = struct.unpack_from("<I", data, 0)[0]
+    sw = magic not in (0xA1B2C3D4, 0xA1B23C4D, 0xA1B2CD34, 0xA1E2CB12)
+    m = struct.unpack_from(">I" if sw else "<I", data, 0)[0]
+    lt = struct.unpack_from(">I" if sw else "<I", data, 20)[0]
+    hs, extra = (24, 0) if m in (0xA1B2CD34, 0xA1E2CB12) else ((32, 16) if lt in (113, 253) else (16, 0))
+    out, pos = [], 24
+    while len(data) - pos >= hs:
+        cl = (struct.unpack_from(">I" if sw else "<I", data, pos + 8)[0] - extra) & 0xFFFFFFFF
+        if cl == 0 or cl > 1 << 20 or len(data) - pos - hs < cl:
+            break
+        out.append((pos, cl))
+        pos += hs + cl
+    return out
+
+
+def _decoys(n, seed):
+    """Frames whose payloads hold runs of pcap-looking record headers (a
+    capture of a pcap transfer): guessed walks start inside them."""
+    rng = np.random.default_rng(seed)
+    pkts = []
+    for i in range(n):
+        body = b""
+        for _ in range(int(rng.integers(0, 40))):
+            cl = int(rng.integers(1, 24))
+            body += struct.pack("<IIII", i, int(rng.integers(0, 999999)), cl, cl) + rng.bytes(cl)
+        pkts.append(rng.bytes(int(rng.integers(0, 20))) + body + rng.bytes(int(rng.integers(0, 64))))
+    return [p if p else b"x" for p in pkts]
+
+
+def test_record_index_is_the_walk(tmp_path):
+    """The replay reader's record index (windows cut into chunks walked from
+    guessed record starts, spliced onto the exact walk) gives the walk's
+    records exactly, for any window and chunk count: record formats, the
+    end rules (a zero-length record, a truncated last record, a caplen past
+    the 1 MiB buffer), records longer than a window, and payloads full of
+    decoy headers."""
+    pkts = [p for p in T.read_pcap(os.path.join(G, "edge.pcap"))[1] if p]
+    files = []
+    f = str(tmp_path / "full.pcap")
+    T.write_pcap(f, pkts)
+    files.append(f)
+    z = str(tmp_path / "z.pcap")
+    rewrite(pkts[:5] + [b""] + pkts[5:9], z)
+    t = str(tmp_path / "t.pcap")
+    open(t, "wb").write(open(f, "rb").read()[:-3])
+    files += [z, t]
+    for fmt, spec in {"be": dict(endian=">"), "nsec": dict(magic=0xA1B23C4D),
+                      "kuz": dict(magic=0xA1B2CD34, rec_extra=bytes(8)),
+                      "bkm_be": dict(magic=0xA1E2CB12, endian=">", rec_extra=bytes(8)),
+                      "sll": dict(linktype=113, ll=True)}.items():
+        g = str(tmp_path / (fmt + ".pcap"))
+        rewrite(pkts[:60], g, **spec)
+        files.append(g)
+    d = str(tmp_path / "decoys.pcap")
+    T.write_pcap(d, _decoys(400, 7))
+    files.append(d)
+    bigf = str(tmp_path / "big.pcap")
+    T.write_pcap(bigf, pkts[:3] + [bytes(70000)] + pkts[3:20] + [bytes(1 << 20)] + pkts[20:30])
+    files.append(bigf)
+    over = str(tmp_path / "over.pcap")
+    T.write_pcap(over, pkts[:10] + [bytes((1 << 20) + 1)] + pkts[10:20])
+    files.append(over)
+    files += [os.path.join(G, n) for n in sorted(os.listdir(G)) if n.endswith(".pcap")]
+    for path in files:
+        want = _walk(path)
+        for window in (1, 7, 100, 999, 4096, 1 << 20, 0):
+            for chunks in (1, 2, 3, 5, 17):
+                off, cap = nsd.pcap_index(path, window, chunks)
+                got = list(zip(off.tolist(), cap.tolist()))
+                assert got == want, (path, window, chunks)
+    with pytest.raises(nsd.NsdError):
+        nsd.pcap_index(str(tmp_path / "missing.pcap"))
+
+
 MODES = [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX, T.PRINT_ASCII, T.PRINT_HEX_ASCII]
 
 
@@ -219,8 +297,8 @@ def test_replay_edge_matches_golden(tmp_path, mode):
 
 @pytest.mark.gpu
 def test_replay_read_paths(tmp_path, monkeypatch):
-    """The replay's two readers give the same text: the mapped file (header
-    scan on the reader, bodies copied by the pool, several pool sizes), the
+    """The replay's two readers give the same text: the mapped file (record
+    index and bodies on the pool, several pool sizes and index windows), the
     read() path (NSD_PCAP_MMAP=0) and a named pipe."""
     path, keep = replayable("edge", T.PRINT_NORM, tmp_path)
     pkts = [p for p in T.read_pcap(path)[1]]
@@ -233,6 +311,12 @@ def test_replay_read_paths(tmp_path, monkeypatch):
         monkeypatch.setenv("NSD_PCAP_MMAP", "0")
         assert nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=4) == (n0, ref)
         monkeypatch.delenv("NSD_PCAP_MMAP")
+        # record index windows of a few records (many windows, each built on
+        # the pool while the one before is scanned, batches cut at windows)
+        for w in ("777", "65536"):
+            monkeypatch.setenv("NSD_PCAP_IX_WINDOW", w)
+            assert nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=5) == (n0, ref)
+        monkeypatch.delenv("NSD_PCAP_IX_WINDOW")
     fifo = str(tmp_path / "p.pcap")
     t = _fifo_feed(fifo, open(big, "rb").read())
     assert nsd.replay_pcap(fifo, mode=T.PRINT_NORM, threads=4) == (n0, ref)
