@@ -52,6 +52,13 @@ struct Out {
 			s.append(buf, (size_t)(w - buf));
 		w = buf;
 	}
+	// the text so far, and dropping what came after `mark` of it
+	size_t size() const { return s.size() + (size_t)(w - buf); }
+	void cut(size_t mark)
+	{
+		flush();
+		s.resize(mark);
+	}
 	// room for n <= sizeof(buf) bytes at w
 	char *room(size_t n)
 	{
@@ -1229,10 +1236,9 @@ int format_packet(std::string &s, const uint8_t *pkt, uint32_t caplen, int linkt
 }
 
 // the same over compact record i: the layer starts come from the prints
-int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
-			  const nsd_crec &rec, uint32_t i, const uint32_t *ext_pool, const nsd_sll_t *sll)
+static int packet_compact(Out &o, const uint8_t *pkt, uint32_t caplen, int linktype, int mode, const nsd_crec &rec,
+			  uint32_t i, const uint32_t *ext_pool, const nsd_sll_t *sll)
 {
-	Out o(s);
 	Frame f{ pkt, caplen };
 	if (format_no_chain(o, f, caplen, mode))
 		return NSD_OK;
@@ -1264,6 +1270,13 @@ int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, i
 		ids[k] = (uint8_t)((rec.chain >> (5 * k)) & 31);
 	return format_chain(o, f, linktype, mode, n, ids, nullptr, nullptr, rec.ip_csum, rec.nflags, sll,
 			    le ? ext_pool[i] & 0xFFFF : 0xFFFFFFFFu);
+}
+
+int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
+			  const nsd_crec &rec, uint32_t i, const uint32_t *ext_pool, const nsd_sll_t *sll)
+{
+	Out o(s);
+	return packet_compact(o, pkt, caplen, linktype, mode, rec, i, ext_pool, sll);
 }
 
 // hex() / ascii() / hex_ascii() over [from, to) (proto_none.c:28-72)
@@ -1311,8 +1324,8 @@ static const char *if_name(uint32_t idx)
 	return last_name->empty() ? nullptr : last_name->c_str();
 }
 
-void format_frame_hdr(std::string &s, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, const uint8_t *pkt,
-		      uint32_t caplen, int linktype, int mode, uint64_t count)
+static void frame_hdr(Out &o, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, const uint8_t *pkt, uint32_t caplen,
+		      int linktype, int mode, uint64_t count)
 {
 	// packet_types[] (dissector.h:31-39)
 	static const char *const types[8] = { "<", "B", "M", "P", ">", nullptr, "K->U", "U->K" };
@@ -1329,7 +1342,6 @@ void format_frame_hdr(std::string &s, const nsd_frame_hdr_t &fh, const nsd_sll_t
 	}
 	const char *pt = pkttype < 8 && types[pkttype] ? types[pkttype] : "?";
 	const char *ifn = if_name(sll ? (uint32_t)sll->ifindex : 0);
-	Out o(s);
 	o << pt;
 	o.c(' ') << (ifn ? ifn : "?");
 	o.c(' ').u(fh.len);
@@ -1365,6 +1377,46 @@ void format_frame_hdr(std::string &s, const nsd_frame_hdr_t &fh, const nsd_sll_t
 		o.u(tci & 0x0fffu) << "), Proto (0x";
 		o.xn(tpid, 4) << ") ]\n";
 	}
+}
+
+void format_frame_hdr(std::string &s, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, const uint8_t *pkt,
+		      uint32_t caplen, int linktype, int mode, uint64_t count)
+{
+	Out o(s);
+	frame_hdr(o, fh, sll, pkt, caplen, linktype, mode, count);
+}
+
+int render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
+		      const nsd_sll_t *sll);
+
+// The replay's formatter job (netsniff-ng.c:732-737 per record): packets
+// [lo, hi) of a batch, show_frame_hdr then the entry point's text, into s
+// through one sink.  A record that could not hold its chain (NSD_F_OVERFLOW:
+// more than NSD_EXT_MAX_LAYERS layers, or the ext pool was full) is rendered
+// by the per-packet path, which has no layer budget; any other status is an
+// error.
+int format_replay_part(std::string &s, const uint8_t *frames, const nsd_desc_t *desc, const nsd_frame_hdr_t *fh,
+		       const nsd_sll_t *sll, const nsd_crec *rec, const uint32_t *ext, uint64_t count0, uint32_t lo,
+		       uint32_t hi, int linktype, int mode)
+{
+	Out o(s);
+	for (uint32_t k = lo; k < hi; k++) {
+		const uint64_t d = desc[k];
+		const uint8_t *const pkt = frames + NSD_DESC_OFF(d);
+		const uint32_t caplen = (uint32_t)NSD_DESC_CAPLEN(d);
+		frame_hdr(o, fh[k], sll + k, pkt, caplen, linktype, mode, count0 + k);
+		const size_t mark = o.size();
+		const int r = packet_compact(o, pkt, caplen, linktype, mode, rec[k], k, ext, sll + k);
+		if (r == NSD_OK)
+			continue;
+		if (!(rec[k].nflags & NSD_F_OVERFLOW))
+			return NSD_ERR_FORMAT;
+		o.cut(mark);
+		const int r2 = render_packet_cpu(s, pkt, caplen, linktype, mode, sll + k);
+		if (r2 != NSD_OK)
+			return r2;
+	}
+	return NSD_OK;
 }
 
 } // namespace nsd
@@ -1479,18 +1531,21 @@ extern "C" long nsd_format_range_compact_fh(const uint8_t *frames, const nsd_des
 	static thread_local std::string t_buf;
 	std::string &s = t_buf;
 	s.clear();
-	for (uint32_t i = lo; i < hi; i++) {
-		const uint64_t d = desc[i];
-		const uint8_t *pkt = frames + NSD_DESC_OFF(d);
-		if (fh)
-			nsd::format_frame_hdr(s, fh[i], sll ? sll + i : nullptr, pkt, NSD_DESC_CAPLEN(d), linktype, mode,
-					      first_count + i);
-		int r = nsd::format_packet_compact(s, pkt, NSD_DESC_CAPLEN(d), linktype, mode, crec[i], i, ext_pool,
-						   sll ? sll + i : nullptr);
-		if (rc)
-			rc[i - lo] = (int8_t)r;
-		if (ends)
-			ends[i - lo] = s.size();
+	{
+		nsd::Out o(s);
+		for (uint32_t i = lo; i < hi; i++) {
+			const uint64_t d = desc[i];
+			const uint8_t *pkt = frames + NSD_DESC_OFF(d);
+			if (fh)
+				nsd::frame_hdr(o, fh[i], sll ? sll + i : nullptr, pkt, NSD_DESC_CAPLEN(d), linktype, mode,
+					       first_count + i);
+			int r = nsd::packet_compact(o, pkt, NSD_DESC_CAPLEN(d), linktype, mode, crec[i], i, ext_pool,
+						    sll ? sll + i : nullptr);
+			if (rc)
+				rc[i - lo] = (int8_t)r;
+			if (ends)
+				ends[i - lo] = o.size();
+		}
 	}
 	const long total = (long)s.size();
 	if (s.size() <= cap)

@@ -55,6 +55,9 @@ void format_frame_hdr(std::string &s, const nsd_frame_hdr_t &fh, const nsd_sll_t
 		      uint32_t caplen, int linktype, int mode, uint64_t count);
 int render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int linktype, int mode,
 		      const nsd_sll_t *sll);
+int format_replay_part(std::string &s, const uint8_t *frames, const nsd_desc_t *desc, const nsd_frame_hdr_t *fh,
+		       const nsd_sll_t *sll, const nsd_crec *rec, const uint32_t *ext, uint64_t count0, uint32_t lo,
+		       uint32_t hi, int linktype, int mode);
 int format_packet_compact(std::string &s, const uint8_t *pkt, uint32_t caplen, int linktype, int mode,
 			  const nsd_crec &rec, uint32_t i, const uint32_t *ext_pool, const nsd_sll_t *sll);
 void cpu_count_packet(const uint8_t *pkt, uint32_t caplen, int linktype, int mode, const nsd_sll_t *sll,
@@ -1075,39 +1078,9 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	// formatter pool: part t of a slot = its packets [n t / parts, n (t+1) / parts)
 	auto render = [&](Slot &x, int t) -> long {
 		const uint32_t lo = (uint32_t)((uint64_t)x.n * t / x.parts), hi = (uint32_t)((uint64_t)x.n * (t + 1) / x.parts);
-		// (locals: appends through a char * would reload every captured field)
-		const uint8_t *const frames = x.frames;
-		const nsd_desc_t *const desc = x.desc;
-		const nsd_frame_hdr_t *const fh = x.fh;
-		const nsd_sll_t *const sll = x.sll;
-		const nsd_crec *const rec = x.rec;
-		const uint32_t *const ext = x.ext;
-		const uint64_t count0 = x.count0;
-		const int lt_ = lt, mode_ = mode;
 		std::string &s = (*x.part)[t].s;
 		s.clear();
-		for (uint32_t k = lo; k < hi; k++) {
-			const uint64_t d = desc[k];
-			const uint8_t *const pkt = frames + NSD_DESC_OFF(d);
-			const uint32_t caplen = (uint32_t)NSD_DESC_CAPLEN(d);
-			// show_frame_hdr, then the entry point (netsniff-ng.c:732-737)
-			nsd::format_frame_hdr(s, fh[k], sll + k, pkt, caplen, lt_, mode_, count0 + k);
-			const size_t mark = s.size();
-			const int r = nsd::format_packet_compact(s, pkt, caplen, lt_, mode_, rec[k], k, ext, sll + k);
-			if (r == NSD_OK)
-				continue;
-			// a record that could not hold its chain (NSD_F_OVERFLOW: longer
-			// than NSD_EXT_MAX_LAYERS layers, or the ext pool was full) is
-			// rendered by the per-packet path, which has no layer budget;
-			// any other status is an error
-			if (!(rec[k].nflags & NSD_F_OVERFLOW))
-				return NSD_ERR_FORMAT;
-			s.resize(mark);
-			const int r2 = nsd::render_packet_cpu(s, pkt, caplen, lt_, mode_, sll + k);
-			if (r2 != NSD_OK)
-				return r2;
-		}
-		return NSD_OK;
+		return nsd::format_replay_part(s, x.frames, x.desc, x.fh, x.sll, x.rec, x.ext, x.count0, lo, hi, lt, mode);
 	};
 	// copy job `q` of `parts` of a mapped file's batch
 	auto fill_part = [&](Slot &x, int q, int parts) {
