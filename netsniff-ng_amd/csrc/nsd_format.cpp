@@ -202,6 +202,23 @@ static bool lay3_has(uint32_t k)
 	return false;
 }
 
+// each byte value as " %.2x" and "%.2x:" in the low 3 bytes of a word
+// (little endian: stored as 4 bytes, the next store 3 further on overwrites
+// the 4th)
+struct HexText {
+	uint32_t sp[256], colon[256];
+	constexpr HexText() : sp(), colon()
+	{
+		const char hx[] = "0123456789abcdef";
+		for (int v = 0; v < 256; v++) {
+			const uint32_t hi = (uint8_t)hx[v >> 4], lo = (uint8_t)hx[v & 15];
+			sp[v] = (uint32_t)' ' | hi << 8 | lo << 16;
+			colon[v] = hi | lo << 8 | (uint32_t)':' << 16;
+		}
+	}
+};
+static constexpr HexText k_hex{};
+
 // decimal text of each octet value, its length in the 4th byte
 struct OctetText {
 	char t[256][4];
@@ -257,16 +274,10 @@ static const char *ether_class(const Frame &f, uint32_t mac)
 // "%.2x:%.2x:%.2x:%.2x:%.2x:%.2x" in one write
 static void mac(Out &o, const Frame &f, uint32_t m)
 {
-	static const char hx[] = "0123456789abcdef";
-	char *w = o.room(17);
-	for (int i = 0; i < 6; i++) {
-		const uint8_t b = f.b(m + i);
-		if (i)
-			*w++ = ':';
-		*w++ = hx[b >> 4];
-		*w++ = hx[b & 15];
-	}
-	o.w = w;
+	char *w = o.room(20);   // (4-byte stores, 3 apart; the 6th ':' is not kept)
+	for (int i = 0; i < 6; i++)
+		memcpy(w + 3 * i, &k_hex.colon[f.b(m + i)], 4);
+	o.w = w + 17;
 }
 
 // ---- layers --------------------------------------------------------------
@@ -1036,19 +1047,16 @@ static void dump_ascii(Out &o, const Frame &f, uint32_t from, uint32_t len)
 
 static void dump_hex(Out &o, const Frame &f, uint32_t from, uint32_t len)
 {
-	static const char hx[] = "0123456789abcdef";
 	if (!len)
 		return;
 	o << " [ Hex ";
 	const bool inside = (uint64_t)from + len <= f.caplen;   // (bytes past caplen read as zero)
 	for (uint32_t i0 = 0; i0 < len; i0 += 512) {
 		const uint32_t m = len - i0 < 512 ? len - i0 : 512;
-		char *w = o.room(3 * (size_t)m);
+		char *w = o.room(3 * (size_t)m + 1);   // (4-byte stores, 3 apart)
 		for (uint32_t i = 0; i < m; i++) {
 			const uint8_t c = inside ? f.p[from + i0 + i] : f.b(from + i0 + i);
-			w[3 * i] = ' ';
-			w[3 * i + 1] = hx[c >> 4];
-			w[3 * i + 2] = hx[c & 15];
+			memcpy(w + 3 * i, &k_hex.sp[c], 4);
 		}
 		o.w += 3 * (size_t)m;
 	}
