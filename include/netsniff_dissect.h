@@ -559,8 +559,9 @@ long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_
 long nsd_pcap_read_batch_fh(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
 			    nsd_sll_t *sll, nsd_frame_hdr_t *fh, uint32_t max_n);
 void nsd_pcap_close(nsd_pcap *p);
-/* nsd_pcap_index: a mapped pcap file's record walk as the replay reader
- * builds it (windows of `window` bytes, 0 = the replay's; each cut into
+/* nsd_pcap_index: a mapped pcap file's record walk (the one read_pcap's
+ * readers take record by record, pcap_mm.c:67 pcap_mm_read) as the replay
+ * reader builds it (windows of `window` bytes, 0 = the replay's; each cut into
  * `chunks` walked in parallel from guessed record starts and spliced onto
  * the exact walk): the first max_n records' header offsets and caplens.
  * Returns the records found (read_batch's end rule) or NSD_ERR_ARG. */
