@@ -22,9 +22,12 @@ def main():
     ap.add_argument("--threads", default="1,2,4,8,16")
     ap.add_argument("--cfg", type=int, default=1)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--lib", default="", help="a variant libnsdissect.so")
     args = ap.parse_args()
     os.environ["NSD_REPLAY_STATS"] = "1"
     import nsd
+    if args.lib:
+        nsd.LIB_PATH = os.path.abspath(args.lib)
     import nsd_testlib as T
     fd = os.open(os.devnull, os.O_WRONLY)
     with tempfile.TemporaryDirectory() as d:
