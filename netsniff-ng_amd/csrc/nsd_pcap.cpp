@@ -973,9 +973,6 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		std::vector<TextPart> *part = nullptr;   // res.part[slot]
 		long prc = NSD_OK;         // first render error
 	};
-	// render jobs per formatter thread and batch (fill jobs wait for the
-	// render job in hand)
-	const int split = getenv("NSD_REPLAY_SPLIT") ? std::max(1, atoi(getenv("NSD_REPLAY_SPLIT"))) : 1;
 	std::vector<Slot> b(NSLOT);
 	std::vector<uint32_t> verdicts(filter ? (size_t)NSLOT * BATCH : 0);
 	std::vector<uint8_t> rhdrs(pcap_fd >= 0 ? (size_t)NSLOT * BATCH * 32 : 0);
@@ -991,8 +988,8 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 		x.verdict = filter ? &verdicts[(size_t)k * BATCH] : nullptr;
 		x.rhdr = pcap_fd >= 0 ? &rhdrs[(size_t)k * BATCH * 32] : nullptr;
 		x.part = &res.part[k];
-		if (x.part->size() < (size_t)(threads * split))
-			x.part->resize((size_t)(threads * split));
+		if (x.part->size() < (size_t)threads)
+			x.part->resize(threads);
 	}
 
 	std::mutex mu;
@@ -1245,7 +1242,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 			for (int c = 0; c < NSD_NCOUNTERS; c++)
 				counters[c] += x.cnt[c];
 		std::lock_guard<std::mutex> g(mu);
-		x.parts = x.n < 2048 ? 1 : (int)std::min<uint32_t>((uint32_t)(threads * split), x.n / 1024);
+		x.parts = x.n < 2048 ? 1 : threads;
 		x.left = x.parts;
 		x.prc = r;
 		x.seq = next_seq++;
