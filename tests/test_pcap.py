@@ -304,8 +304,13 @@ def test_replay_read_paths(tmp_path, monkeypatch):
     pkts = [p for p in T.read_pcap(path)[1]]
     big = str(tmp_path / "big.pcap")
     T.write_pcap(big, pkts * 600)   # > one 65536-record batch
-    for pth in (path, big):
+    decoys = str(tmp_path / "decoys.pcap")
+    T.write_pcap(decoys, _decoys(3000, 11))   # guessed index walks start in payloads
+    for pth in (decoys, path, big):
+        monkeypatch.setenv("NSD_PCAP_MMAP", "0")
         n0, ref = nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=1)
+        monkeypatch.delenv("NSD_PCAP_MMAP")
+        assert nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=1) == (n0, ref)
         for th in (2, 5, 16):
             assert nsd.replay_pcap(pth, mode=T.PRINT_NORM, threads=th) == (n0, ref)
         monkeypatch.setenv("NSD_PCAP_MMAP", "0")
