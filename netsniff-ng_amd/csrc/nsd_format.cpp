@@ -150,7 +150,7 @@ struct Out {
 		int k = (bits + 3) >> 2;
 		if (k < n)
 			k = n;
-		char *p = room(16 + (size_t)(n > 16 ? n - 16 : 0));
+		char *p = room((size_t)k);
 		w = p + k;
 		for (int i = k - 1; i >= 0; i--, v >>= 4)
 			p[i] = hx[v & 15];
