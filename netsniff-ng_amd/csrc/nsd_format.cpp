@@ -1337,6 +1337,7 @@ static void frame_hdr(Out &o, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, c
 {
 	// packet_types[] (dissector.h:31-39)
 	static const char *const types[8] = { "<", "B", "M", "P", ">", nullptr, "K->U", "U->K" };
+	static const uint8_t type_len[8] = { 1, 1, 1, 1, 1, 0, 4, 4 };
 	if (mode == PRINT_NONE)
 		return;
 	uint8_t pkttype = sll ? sll->pkttype : 0;
@@ -1348,17 +1349,23 @@ static void frame_hdr(Out &o, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, c
 		memcpy(&pid, pkt + 12, 4);
 		pkttype = pid == 0 ? 7 : 6;
 	}
-	const char *pt = pkttype < 8 && types[pkttype] ? types[pkttype] : "?";
+	if (pkttype < 8 && types[pkttype])
+		o.put(types[pkttype], type_len[pkttype]);
+	else
+		o << "?";
 	const char *ifn = if_name(sll ? (uint32_t)sll->ifindex : 0);
-	o << pt;
-	o.c(' ') << (ifn ? ifn : "?");
-	o.c(' ').u(fh.len);
+	if (ifn)
+		o << " " << ifn << " ";
+	else
+		o << " ? ";
+	o.u(fh.len);
 	if (mode == PRINT_LESS) {
 		o << " #";
 		o.u(count);
 		return;
 	}
-	o.c(' ').u(fh.sec) << "s.";
+	o << " ";
+	o.u(fh.sec) << "s.";
 	o.u(fh.nsec) << "ns #";
 	o.u(count).c(' ');
 	if (!fh.v3) {
