@@ -12,16 +12,25 @@ times the 16-byte nsd_rec; the other form is measured beside it
 walks S contiguous 16M shards of the same stream as one batch on one GPU
 (--config imix --shards 8 = C5's 128M packets on a single MI355X).
 
-The same run also measures, beside the headline (rank 0, N = 1):
-  legs        C3 (IMIX; the metric is "64B & IMIX") and C4 as their own
-              measured objects (kernel time, roofline, traffic);
+At every N (rank r walks its own 16M-packet shard [r * 16M, (r + 1) * 16M)
+of each config; the counter vector is all-reduced over the ranks inside the
+timed region and checked against the oracle's per-shard counters,
+tests/golden/shard_counters.json):
+  headline    C2 (or --config), `value` = whole-job Mpkt/s, per-GPU roofline;
+  legs        C3 IMIX (the metric is "64B & IMIX"; at N = 8 its shards are
+              C5's 128M IMIX packets across 8 GPUs) and C4, each with its
+              whole-job rate, per-GPU kernel time and roofline.
+Beside them, at N = 1 only:
   traffic     HBM bytes per launch from rocprofv3 PMC counters, collected
               in-run by two child processes (FETCH_SIZE and WRITE_SIZE in
               separate passes, MI355X_MICROARCH.md "HBM") before this
               process touches the GPU;
+  other_records the other record form over the headline workload;
   cpu_baseline the CPU restatement (oracle, "port") on this host's cores:
               fields + text (what the reference does: it prints as it
-              parses) and fields only, 1 thread and all threads;
+              parses) and fields only, 1 thread and all threads; and the
+              reference's own objects (oracle/_ref/nsref) on one core and
+              as one process per core of the 16-CPU share, C2 and C3;
   end_to_end / replay / bpf_filter (reported, never `value`).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
@@ -459,12 +468,56 @@ def ref_harness_rate(cfg, key, n=1 << 17, frames=True):
                       f"included"}
 
 
+def ref_harness_all_cores(cfg, key, procs, rate1, seconds=8.0):
+    """The reference's own objects on `procs` host cores at once, the way
+    the reference scales a capture out (one netsniff-ng process per CPU in
+    a PACKET_FANOUT group, ring_rx.c:197-215; the `--in` loop,
+    netsniff-ng.c:707-756): `procs` oracle/_ref/nsref -f processes, each over
+    its own contiguous shard of the workload as a pcap file (records
+    [p * n, (p + 1) * n)), started together, text to /dev/null.  n is sized
+    from the one-core rate `rate1` (Mpkt/s) for about `seconds` of work per
+    process.  Rate = all records / the wall time from the first start to the
+    last exit (process start included).  None when the harness was not
+    built."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "nsref")
+    if not os.path.exists(exe) or not rate1:
+        return None
+    from concurrent.futures import ThreadPoolExecutor
+    n = int(min(max(rate1 * 1e6 * seconds, 4096), 1 << 20))
+    with tempfile.TemporaryDirectory() as d:
+        paths = [os.path.join(d, f"shard{p}.pcap") for p in range(procs)]
+        with ThreadPoolExecutor(procs) as ex:
+            list(ex.map(lambda p: T.synth().nsd_synth_pcap(cfg, T.SEED, p * n, n, paths[p].encode()),
+                        range(procs)))
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen([exe, "-f", "-m", str(T.PRINT_NORM), "-w", "0", "-i", paths[p] + ".idx", paths[p]],
+                               stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+              for p in range(procs)]
+        errs = []
+        for pr in ps:
+            _, e = pr.communicate(timeout=600)
+            if pr.returncode != 0:
+                errs.append(f"rc={pr.returncode}: {e.decode(errors='replace')[-120:]}")
+        dt = time.perf_counter() - t0
+    if errs:
+        return {"error": "; ".join(errs[:2])}
+    return {"value": round(procs * n / dt / 1e6, 4), "unit": "Mpkt/s", "cores": procs, "processes": procs,
+            "kind": "reference",
+            "sample": f"{key}: {procs} concurrent `nsref -f` processes (the reference's pcap reader, record "
+                      f"conversion, frame header line, parser objects and tprintf.c at 80 columns; IPv4/IPv6 "
+                      f"restated), each over its own {n}-record contiguous shard, text to /dev/null, "
+                      f"{procs * n} records in {dt:.2f} s wall, process start included",
+            "vs_1core": round(procs * n / dt / 1e6 / rate1, 2)}
+
+
 def cpu_baseline(key, seconds):
     """The CPU restatement on this host (SURVEY 8d / BASELINE.md "CPU-baseline
     plan"): fields + PRINT_NORM text and fields only, each on 1 thread, on
     the GPU's 16-thread CPU share and on every available core.  `value` is
     the text rate on all available cores (what the reference does - it
-    prints as it parses - on the whole host), `cores` that thread count."""
+    prints as it parses - on the whole host), `cores` that thread count.
+    Beside it, the reference's own objects (oracle/_ref/nsref) on one core
+    and as one process per core of the same share, for C2 and C3 IMIX."""
     cfg = CONFIGS[key]["cfg"]
     model, nproc, avail = cpu_info()
     t16 = min(avail, 16)   # the GPU box's CPU share per GPU is 16 threads
@@ -479,6 +532,12 @@ def cpu_baseline(key, seconds):
         fA, qA, eA = cpu_rate(cfg, max(1 << 22, 65536 * avail), avail, seconds / legs, False)
     else:
         tA, pA, dA, fA = tS, pS, dS, fS
+    ref1, refA = {}, {}
+    for k in ("udp64", "imix"):
+        r1 = ref_harness_rate(CONFIGS[k]["cfg"], k, n=(1 << 17) if k == "udp64" else (1 << 15))
+        ref1[k] = r1
+        refA[k] = ref_harness_all_cores(CONFIGS[k]["cfg"], k, t16,
+                                        r1.get("value") if isinstance(r1, dict) else None)
     return {"value": round(tA, 3), "unit": "Mpkt/s", "cores": avail, "kind": "port",
             "sample": f"{key}: fields + PRINT_NORM text with frame header lines (the reference prints as "
                       f"it parses; `netsniff-ng --in`'s text) by the CPU "
@@ -491,7 +550,9 @@ def cpu_baseline(key, seconds):
             "fields_only": {"all_cores": round(fA, 3), "threads16": round(fS, 3), "1thread": round(f1, 3)},
             "reference_harness_container": "0.182 Mpkt/s PRINT_NORM 1 core (BASELINE.md, measured in the "
                                            "build container, not on this host)",
-            "reference_harness_1thread": ref_harness_rate(cfg, key),
+            "reference_harness_1thread": ref1.get(key, ref1["udp64"]),
+            "reference_harness_1thread_by_workload": ref1,
+            "reference_harness_all_cores": refA,
             "reference_dissector_1thread": ref_harness_rate(cfg, key, frames=False)}
 
 
@@ -747,6 +808,63 @@ def measure_rank(args, rank, world, dev, engine="device"):
                "accumulate": accumulate, "frame_bytes": b.frame_bytes}
 
 
+
+SHARD_COUNTERS = os.path.join(ROOT, "tests", "golden", "shard_counters.json")
+
+
+def golden_counters(key, n, world, shards=1):
+    """The oracle's PRINT_NORM counter vector summed over the shards the
+    `world` ranks walk (rank r: packets [r * n * shards, (r + 1) * n * shards)
+    in n-packet shards; tests/golden/shard_counters.json, made by
+    make_golden.py --shards-only), or None when the table lacks a shard."""
+    if not os.path.exists(SHARD_COUNTERS):
+        return None
+    with open(SHARD_COUNTERS) as f:
+        table = json.load(f)
+    total = np.zeros(nsd.NCOUNTERS, dtype=np.uint64)
+    for j in range(world * shards):
+        k = f"{key}:{j * n}:{n}"
+        if k not in table:
+            return None
+        total += np.array(table[k], dtype=np.uint64)
+    return total
+
+
+def workload_name_n(key, n, shards, world):
+    if world > 1 and key == "imix" and shards == 1:
+        tag = "C5" if world == 8 else "C5-style"
+        return (f"{tag}: {world * n} IMIX packets sharded across {world} GPUs "
+                f"({n // (1 << 20)}M per GPU, counters all-reduced)")
+    name = workload_name(key, n, shards)
+    return name if world == 1 else f"{name}, {world} GPUs x {n * shards} packets"
+
+
+def workload_result(args, key, b, m, world, engine, traffic=None, copy_gbs=None, ceiling=None):
+    """One workload of the line, measured by measure_rank at this N: the
+    whole-job rate (wall clock, max over ranks, counter all-reduce inside),
+    the per-GPU kernel time and roofline, and the all-reduced counters
+    checked against the oracle's per-shard counters (a mismatch fails the
+    run)."""
+    elapsed, kern_ms, total = m["elapsed"], m["kern_ms"], m["total_pkts"]
+    reps = args.steps if m["accumulate"] else 1
+    want = golden_counters(key, b.n_shard, world, b.shards) if engine == "device" else None
+    if want is not None:
+        assert np.array_equal(m["counters"], want * np.uint64(reps)), \
+            f"{key}: all-reduced counters differ from the oracle's shard counters"
+    tr = traffic.get(key) if isinstance(traffic, dict) else None
+    return {"workload": workload_name_n(key, b.n_shard, b.shards, world), "packets": total,
+            "packets_per_gpu": b.n, "schedule": nsd.last_schedule() if engine == "device" else "host walk",
+            "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "Mpkt/s",
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "kernel_value": round(total / (kern_ms * 1e-3) / 1e6, 2),
+            "gbps_frames": round(m["frame_bytes"] * world * args.steps / elapsed / 1e9, 1),
+            "roofline": b.roofline(kern_ms, tr, copy_gbs, ceiling),
+            "counters": nsd.unpack_counters(m["counters"]),
+            "counters_check": (f"all-reduced over {world} rank(s) = the oracle's counters of the {world * b.shards} "
+                               f"shard(s) x {reps} launch(es) (tests/golden/shard_counters.json)")
+            if want is not None else "packets = ranks x shard x launches (no golden for this shard size)"}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -775,6 +893,129 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def run(args, rank, world, dev, engine="device", traffic=None):
+    """Every rank's measurements in launch order (the same collectives on
+    every rank), and rank 0's JSON line (a dict; None on other ranks).  At
+    every N: the headline workload and each leg (C3 IMIX, whose 8-rank run is
+    C5, and C4) through measure_rank, the counters all-reduced and checked
+    against the oracle's per-shard counters.  N = 1 only: the other record
+    form, the CPU baseline, end to end, replay and BPF.  engine "host"
+    (tests/test_multi.py) walks each shard with the product's host walk and
+    skips the device-only legs."""
+    solo = rank == 0 and world == 1
+    dev_eng = engine == "device"
+    legs = [k for k in LEGS if k != args.config] if not args.no_legs else []
+    n = args.packets
+    compact = args.records == "compact"
+
+    b, m = measure_rank(args, rank, world, dev, engine)
+    schedule = nsd.last_schedule() if dev_eng else "host walk"
+    elapsed, kern_ms, total_pkts = m["elapsed"], m["kern_ms"], m["total_pkts"]
+    ms_per_step = elapsed / args.steps * 1e3
+    mpps = total_pkts * args.steps / elapsed / 1e6
+
+    copy_gbs = copy_rate(dev) if dev_eng else None
+    ceiling = read_ceiling(b.frames) if dev_eng else None
+    head = workload_result(args, args.config, b, m, world, engine, traffic, copy_gbs, ceiling)
+    roofline = head["roofline"]
+    # the BPF leg filters C3's IMIX (its "IPv4 TCP" program accepts the
+    # untagged TCP sixth; C2's UDP would leave the compaction nothing)
+    want_bpf = solo and dev_eng and not args.no_bpf
+    bpf = bpf_bench(b, args.steps, args.warmup) if want_bpf and (args.config == "imix" or "imix" not in legs) \
+        else None
+    frame_bytes = b.frame_bytes
+    b.free()
+    if dev_eng:
+        torch.cuda.empty_cache()
+
+    # the other record form over the same workload (kernel time, roofline)
+    other = None
+    if solo and dev_eng and not args.no_legs:
+        ob = Batch(args.config, n, 0, args.shards, dev, compact=not compact)
+        oms = time_steps(ob, args.mode, args.steps, args.warmup, 0)
+        other = {"records": "full 16 B (nsd_rec)" if compact else "compact 8 B (nsd_crec)",
+                 "value": round(ob.n / (oms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
+                 "roofline": ob.roofline(oms, None, copy_gbs, ceiling)}
+        ob.free()
+        torch.cuda.empty_cache()
+    if roofline is not None:
+        # which of SURVEY 8(a)'s chain-walk fields the timed launches write
+        if compact:
+            roofline["record_form"] = ("compact 8 B nsd_crec: ops-id chain, IPv4 checksum, layer count + flags "
+                                       "(side word / ext entry past 6 layers); the per-layer offsets and the "
+                                       "final data/tail cursor are re-derived by the renderer, not written")
+        else:
+            roofline["record_form"] = ("full 16 B nsd_rec: ops-id chain, per-layer offsets, final data/tail "
+                                       "cursor, IPv4 checksum, layer count + flags")
+        if other is not None and other["roofline"] is not None:
+            roofline["other_record_form"] = {"records": other["records"],
+                                             "frac": other["roofline"]["frac"],
+                                             "read_frac": other["roofline"]["read_frac"],
+                                             "kernel_ms": other["roofline"]["kernel_ms"]}
+
+    # every leg at every N: rank r walks its own 16M shard of each config
+    # (8 IMIX ranks = C5's 128M packets), counters all-reduced and checked
+    leg_out = {}
+    for key in legs:
+        la = argparse.Namespace(**vars(args))
+        la.config, la.shards = key, 1
+        lb, lm = measure_rank(la, rank, world, dev, engine)
+        if key == "imix" and want_bpf and bpf is None:
+            bpf = bpf_bench(lb, args.steps, args.warmup)
+        leg_out[key] = workload_result(la, key, lb, lm, world, engine, traffic, copy_gbs, ceiling)
+        lb.free()
+        if dev_eng:
+            torch.cuda.empty_cache()
+
+    cpu = None
+    if solo and dev_eng and not args.no_cpu:
+        cpu = cpu_baseline(args.config, args.cpu_seconds)
+
+    e2e = None
+    if solo and dev_eng and not args.no_e2e:
+        e2e = end_to_end(CONFIGS[args.config]["cfg"], args.e2e_batch, args.e2e_batches, args.e2e_depth, args.mode)
+
+    replay = None
+    if solo and dev_eng and not args.no_replay:
+        replay = replay_leg(CONFIGS[args.config]["cfg"], args.replay_packets, args.mode, min(cpu_info()[2], 16))
+        if cpu is not None:
+            # the CPU-only text rate on the same thread count
+            replay["cpu_text_same_threads"] = cpu["text_16threads"]["value"]
+            replay["vs_cpu_text_same_threads"] = round(replay["value"] / cpu["text_16threads"]["value"], 3)
+            ref = (cpu.get("reference_harness_all_cores") or {}).get(args.config)
+            if isinstance(ref, dict) and ref.get("value"):
+                replay["reference_same_cores"] = ref["value"]
+                replay["vs_reference_same_cores"] = round(replay["value"] / ref["value"], 2)
+
+    if rank != 0:
+        return None
+    out = {
+        "metric": "Mpkt/s + GB/s device-resident dissect, 64B & IMIX; bit-exact fields vs ref",
+        "value": round(mpps, 2), "unit": "Mpkt/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 generators, tools/nsd_synth.c)",
+        "config": {"workload": workload_name_n(args.config, n, args.shards, world), "packets_per_gpu": n * args.shards,
+                   "frame_bytes_per_gpu": frame_bytes, "mode": MODES[args.mode],
+                   "records": "compact 8 B (nsd_crec)" if compact else "full 16 B (nsd_rec)",
+                   "schedule": schedule, "parallelism": f"dp{world}"},
+        "gbps_frames": round(frame_bytes * world * args.steps / elapsed / 1e9, 1),
+        "roofline": roofline,
+        "counters_total": int(m["counters"][nsd.CNT_PKTS]),
+        "counters_check": head["counters_check"],
+        "legs": leg_out or None,
+        "other_records": other,
+        "cpu_baseline": cpu,
+        "end_to_end": e2e,
+        "replay": replay,
+        "bpf_filter": bpf,
+        "library": library_info() if dev_eng else None,
+    }
+    if isinstance(traffic, dict) and "error" in traffic:
+        out["pmc_error"] = traffic["error"]
+    return out
+
+
 def main():
     args = parse_args()
     if args.pmc_child:
@@ -794,7 +1035,7 @@ def main():
         print(f"bench.py: --gpus {args.gpus} under a launcher of {world} ranks", file=sys.stderr)
         sys.exit(2)
     solo = rank == 0 and world == 1
-    legs = [k for k in LEGS if k != args.config] if solo and not args.no_legs else []
+    legs = [k for k in LEGS if k != args.config] if not args.no_legs else []
 
     # PMC traffic first, in child processes, before this process initialises the GPU
     traffic = None
@@ -806,95 +1047,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
-    n = args.packets
-    compact = args.records == "compact"
-
-    b, m = measure_rank(args, rank, world, dev)
-    schedule = nsd.last_schedule()   # the kernel schedule the timed launches ran (adaptive)
-    elapsed, kern_ms, total_pkts = m["elapsed"], m["kern_ms"], m["total_pkts"]
-    ms_per_step = elapsed / args.steps * 1e3
-    mpps = total_pkts * args.steps / elapsed / 1e6
-
-    copy_gbs = copy_rate(dev)
-    ceiling = read_ceiling(b.frames)
-    tr = traffic.get(args.config) if isinstance(traffic, dict) else None
-    roofline = b.roofline(kern_ms, tr, copy_gbs, ceiling)
-    # the BPF leg filters C3's IMIX (its "IPv4 TCP" program accepts the
-    # untagged TCP sixth; C2's UDP would leave the compaction nothing)
-    want_bpf = solo and not args.no_bpf
-    bpf = bpf_bench(b, args.steps, args.warmup) if want_bpf and (args.config == "imix" or "imix" not in legs) \
-        else None
-    frame_bytes = b.frame_bytes
-    b.free()
-    torch.cuda.empty_cache()
-
-    # the other record form over the same workload (kernel time, roofline)
-    other = None
-    if solo and not args.no_legs:
-        ob = Batch(args.config, n, 0, args.shards, dev, compact=not compact)
-        oms = time_steps(ob, args.mode, args.steps, args.warmup, 0)
-        other = {"records": "full 16 B (nsd_rec)" if compact else "compact 8 B (nsd_crec)",
-                 "value": round(ob.n / (oms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
-                 "roofline": ob.roofline(oms, None, copy_gbs, ceiling)}
-        ob.free()
-        torch.cuda.empty_cache()
-
-    leg_out = {}
-    for key in legs:
-        lb = Batch(key, n, 0, 1, dev, compact=compact)
-        ms = time_steps(lb, args.mode, args.steps, args.warmup, args.grid)
-        lc = lb.counters.cpu().numpy().view(np.uint64)
-        assert int(lc[nsd.CNT_PKTS]) == lb.n, f"{key}: counter check failed"
-        if key == "imix" and want_bpf and bpf is None:
-            bpf = bpf_bench(lb, args.steps, args.warmup)
-        ltr = traffic.get(key) if isinstance(traffic, dict) else None
-        leg_out[key] = {"workload": CONFIGS[key]["name"], "packets": lb.n, "schedule": nsd.last_schedule(),
-                        "value": round(lb.n / (ms * 1e-3) / 1e6, 2), "unit": "Mpkt/s (kernel time)",
-                        "gbps_frames": round(lb.frame_bytes / (ms * 1e-3) / 1e9, 1),
-                        "roofline": lb.roofline(ms, ltr, copy_gbs, ceiling)}
-        lb.free()
-        torch.cuda.empty_cache()
-
-    cpu = None
-    if solo and not args.no_cpu:
-        cpu = cpu_baseline(args.config, args.cpu_seconds)
-
-    e2e = None
-    if solo and not args.no_e2e:
-        e2e = end_to_end(CONFIGS[args.config]["cfg"], args.e2e_batch, args.e2e_batches, args.e2e_depth, args.mode)
-
-    replay = None
-    if solo and not args.no_replay:
-        replay = replay_leg(CONFIGS[args.config]["cfg"], args.replay_packets, args.mode, min(cpu_info()[2], 16))
-        if cpu is not None:
-            # the CPU-only text rate on the same thread count
-            replay["cpu_text_same_threads"] = cpu["text_16threads"]["value"]
-            replay["vs_cpu_text_same_threads"] = round(replay["value"] / cpu["text_16threads"]["value"], 3)
-
-    if rank == 0:
-        out = {
-            "metric": "Mpkt/s + GB/s device-resident dissect, 64B & IMIX; bit-exact fields vs ref",
-            "value": round(mpps, 2), "unit": "Mpkt/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (seeded splitmix64 generators, tools/nsd_synth.c)",
-            "config": {"workload": workload_name(args.config, n, args.shards), "packets_per_gpu": b.n,
-                       "frame_bytes_per_gpu": frame_bytes, "mode": MODES[args.mode],
-                       "records": "compact 8 B (nsd_crec)" if compact else "full 16 B (nsd_rec)",
-                       "schedule": schedule, "parallelism": f"dp{world}"},
-            "gbps_frames": round(frame_bytes * world * args.steps / elapsed / 1e9, 1),
-            "roofline": roofline,
-            "counters_total": int(m["counters"][nsd.CNT_PKTS]),
-            "legs": leg_out or None,
-            "other_records": other,
-            "cpu_baseline": cpu,
-            "end_to_end": e2e,
-            "replay": replay,
-            "bpf_filter": bpf,
-            "library": library_info(),
-        }
-        if isinstance(traffic, dict) and "error" in traffic:
-            out["pmc_error"] = traffic["error"]
+    out = run(args, rank, world, dev, "device", traffic)
+    if out is not None:
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist

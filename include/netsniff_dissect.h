@@ -536,7 +536,15 @@ long nsd_format_range_compact_fh(const uint8_t *frames, const nsd_desc_t *desc, 
  * out_fd, in file order (a *_LL file's cooked headers reach the SLL head as
  * each packet's sockaddr_ll); counters (may be NULL) accumulates the counter
  * vector; `threads` host threads format each batch (<= 0: up to 16).
- * Returns the records printed or a negative NSD_ERR_*. */
+ * Returns the records printed or a negative NSD_ERR_*.
+ * A regular file is mapped whole at nsd_pcap_open (pcap_mm.c's way): the
+ * replay is a snapshot of the file as it was at open - records appended
+ * later are not read, and a truncation by another process while it is
+ * replayed faults the reader (SIGBUS), as the reference's mapped reader
+ * would.  NSD_PCAP_MMAP=0 in the environment reads with read() instead
+ * (pcap_sg.c's way: a growing file is followed to its current end).
+ * Interface names (the frame header line) are looked up afresh by each
+ * replay. */
 typedef struct nsd_pcap nsd_pcap;
 struct nsd_bpf_prog;
 nsd_pcap *nsd_pcap_open(const char *path);
@@ -545,8 +553,11 @@ long nsd_pcap_read_batch(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *d
 			 uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns);
 /* as nsd_pcap_read_batch, also filling sll[k] (may be NULL) as read_pcap
  * fills fm.s_ll (netsniff-ng.c:672, 727; pcap_pkthdr_to_tpacket_hdr ->
- * ll_to_sockaddr, pcap_io.h:182-191, 594-660): the *_LL record's cooked
- * header, zeros for other record forms. */
+ * ll_to_sockaddr, pcap_io.h:182-191, 594-660): every sockaddr_ll field that
+ * conversion sets - the *_LL record's cooked header; ifindex / protocol /
+ * pkttype (Kuznetzov); ifindex / protocol / hatype / pkttype (Borkmann) -
+ * and zeros elsewhere (r04: Kuznetzov / Borkmann records used to leave
+ * zeros; read_batch_fh below fills the same fields). */
 long nsd_pcap_read_batch_sll(nsd_pcap *p, uint8_t *frames, size_t cap, nsd_desc_t *desc,
 			     nsd_sll_t *sll, uint32_t max_n, uint32_t *wire_len, uint64_t *ts_ns);
 /* as nsd_pcap_read_batch_sll, also filling fh[k] (may be NULL) with the

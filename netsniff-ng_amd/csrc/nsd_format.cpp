@@ -16,6 +16,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -1307,29 +1308,66 @@ void format_post_dump(std::string &s, const uint8_t *pkt, uint32_t caplen, int m
 // ---- show_frame_hdr (dissector.h:31-116) ----------------------------------
 
 // if_indextoname (dissector.h:82, 89), cached per interface index: the
-// reference asks the kernel for every packet (a socket and an ioctl); the
-// name of an index does not change while a capture runs.  Index 0 names no
-// interface.  Returns nullptr where if_indextoname fails.
-static const char *if_name(uint32_t idx)
+// reference asks the kernel for every packet (a socket and an ioctl).  The
+// lookup runs outside the cache's lock; only names that exist are cached
+// (at most IF_CACHE_MAX indexes: a file of many distinct indexes pays the
+// lookups past that, as the reference does), and a failed lookup is kept
+// only as the thread's last one, so an interface that appears later is
+// seen.  nsd_if_cache_reset() (each replay, dissector_cleanup_all) drops the
+// cache: renamed interfaces are seen by the next replay.  Index 0 names no
+// interface.  Copies the name into b (IF_NAMESIZE bytes); false where there
+// is none.
+namespace {
+constexpr size_t IF_NAME_MAX = 16;   // IF_NAMESIZE
+constexpr size_t IF_CACHE_MAX = 4096;
+std::mutex g_if_mu;
+std::unordered_map<uint32_t, std::string> g_if_names;
+std::atomic<uint32_t> g_if_gen{ 1 };
+} // namespace
+
+extern "C" __attribute__((visibility("hidden"))) void nsd_if_cache_reset(void)
 {
-	static std::mutex mu;
-	static std::unordered_map<uint32_t, std::string> names;   // "" = no such interface
-	thread_local uint32_t last = 0;
-	thread_local const std::string *last_name = nullptr;
+	std::lock_guard<std::mutex> g(g_if_mu);
+	g_if_names.clear();
+	g_if_gen.fetch_add(1, std::memory_order_relaxed);
+}
+
+static bool if_name(uint32_t idx, char *b)
+{
+	thread_local uint32_t t_idx = 0, t_gen = 0;
+	thread_local bool t_ok = false;
+	thread_local char t_name[IF_NAME_MAX];
 	if (idx == 0)
-		return nullptr;
-	if (idx != last || !last_name) {
-		std::lock_guard<std::mutex> g(mu);
-		auto it = names.find(idx);
-		if (it == names.end()) {
-			char b[32];
-			const char *r = if_indextoname(idx, b);
-			it = names.emplace(idx, r ? r : "").first;
-		}
-		last = idx;
-		last_name = &it->second;   // (map nodes do not move)
+		return false;
+	const uint32_t gen = g_if_gen.load(std::memory_order_relaxed);
+	if (idx == t_idx && gen == t_gen) {
+		if (t_ok)
+			memcpy(b, t_name, IF_NAME_MAX);
+		return t_ok;
 	}
-	return last_name->empty() ? nullptr : last_name->c_str();
+	bool ok = false, cached = false;
+	{
+		std::lock_guard<std::mutex> g(g_if_mu);
+		auto it = g_if_names.find(idx);
+		if (it != g_if_names.end()) {
+			snprintf(b, IF_NAME_MAX, "%s", it->second.c_str());
+			ok = cached = true;
+		}
+	}
+	if (!cached) {
+		ok = if_indextoname(idx, b) != nullptr;
+		if (ok) {
+			std::lock_guard<std::mutex> g(g_if_mu);
+			if (g_if_names.size() < IF_CACHE_MAX)
+				g_if_names.emplace(idx, b);
+		}
+	}
+	t_idx = idx;
+	t_gen = gen;
+	t_ok = ok;
+	if (ok)
+		memcpy(t_name, b, IF_NAME_MAX);
+	return ok;
 }
 
 static void frame_hdr(Out &o, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, const uint8_t *pkt, uint32_t caplen,
@@ -1353,9 +1391,9 @@ static void frame_hdr(Out &o, const nsd_frame_hdr_t &fh, const nsd_sll_t *sll, c
 		o.put(types[pkttype], type_len[pkttype]);
 	else
 		o << "?";
-	const char *ifn = if_name(sll ? (uint32_t)sll->ifindex : 0);
-	if (ifn)
-		o << " " << ifn << " ";
+	char ifb[IF_NAME_MAX];
+	if (if_name(sll ? (uint32_t)sll->ifindex : 0, ifb))
+		o << " " << ifb << " ";
 	else
 		o << " ? ";
 	o.u(fh.len);

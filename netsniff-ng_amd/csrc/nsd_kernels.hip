@@ -1978,6 +1978,7 @@ constexpr int MAX_DEV = 16;
 #endif
 struct Sched {
 	bool init = false, fused = false, pending = false, small = false;
+	bool recorded = false;                 // the pending sample's event is recorded (sched_sampled)
 	int launches = 0, last = 0;
 	uint64_t sampled = 0;                  // packets of the sampled launch in flight
 	unsigned long long *host = nullptr;    // its pair, then its counters [32, 34) before and after
@@ -2020,7 +2021,10 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 	// capture; the graph replays this plan)
 	hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
 	const bool capturing = hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
-	if (!capturing && S.pending && hipEventQuery(S.ev) == hipSuccess) {
+	// (a sample is read only once sched_sampled has recorded its event: between
+	// the plan and that record, the event still stands for an older sample, and
+	// another stream's launch must not take the copies in flight for it)
+	if (!capturing && S.pending && S.recorded && hipEventQuery(S.ev) == hipSuccess) {
 		const double rd = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
 		const double ri = S.sampled ? (double)S.host[1] / (double)S.sampled : 0.0;
 		S.fused = S.fused ? rd > 0.05 || ri > 0.05 : rd > 0.15 || ri > 0.10;
@@ -2028,6 +2032,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 		if (pk)
 			S.small = by <= (uint64_t)NSD_SMALL_FRAME * pk;
 		S.pending = false;
+		S.recorded = false;
 	}
 	if (!S.init && !capturing) {
 		S.init = true;
@@ -2044,6 +2049,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 		S.launches = 0;
 		S.sampled = n;
 		S.pending = true;   // (until its copy lands)
+		S.recorded = false;
 	}
 	S.last = p.fused ? NSD_SCHED_FUSED : NSD_SCHED_SPLIT;
 	return p;
@@ -2058,10 +2064,20 @@ void sched_sampled(unsigned long long *pair, const uint64_t *counters, hipStream
 	if (hipMemcpyAsync(S.host, pair, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
 	    hipMemcpyAsync(S.host + 4, counters + NSD_CNT_PKTS, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
 	    hipEventRecord(S.ev, stream) != hipSuccess) {
-		memset(S.host, 0, 48);
-		S.sampled = 0;
-		(void)hipEventRecord(S.ev, nullptr);
+		S.pending = false;   // no sample this time (the copies may still land: nothing reads them)
+		S.recorded = false;
+		return;
 	}
+	S.recorded = true;
+}
+
+// the sampled launch's kernels failed to launch: drop the sample
+void sched_abort()
+{
+	std::lock_guard<std::mutex> g(g_sched_mu);
+	Sched &S = g_sched[cur_dev()];
+	S.pending = false;
+	S.recorded = false;
 }
 } // namespace
 
@@ -2181,8 +2197,11 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	hipLaunchKernelGGL(f, dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec, d_ext,
 			   ext_words, d_ext_used, chunk_for(blocks), (unsigned long long *)d_counters, (uint64_t *)d_ws,
 			   region_for(n, blocks), (const uint32_t *)d_sll, sched);
-	if (hipGetLastError() != hipSuccess)
+	if (hipGetLastError() != hipSuccess) {
+		if (sched)
+			sched_abort();
 		return -2;
+	}
 	if (sched)
 		sched_sampled(sched, d_counters, stream);
 	return 0;
@@ -2224,8 +2243,11 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	uint32_t *side = compact && d_ext && ext_words >= n ? d_ext : nullptr;
 	hipLaunchKernelGGL(fast[ci][mi], dim3(fblocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec,
 			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll, side, sched);
-	if (hipGetLastError() != hipSuccess)
+	if (hipGetLastError() != hipSuccess) {
+		if (sched)
+			sched_abort();
 		return -2;
+	}
 	if (mi == 2)
 		return 0;   // no chains: nothing deferred
 	uint32_t wcap = grid > 0 ? (uint32_t)grid
@@ -2239,8 +2261,11 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	hipLaunchKernelGGL(walk[ci][mi], dim3(wblocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, d_rec, d_ext,
 			   ext_words, d_ext_used, chunk_for(wblocks), (unsigned long long *)d_counters, lists, cap, cnts,
 			   nlists, pend, per_wave * cap * WAVES);
-	if (hipGetLastError() != hipSuccess)
+	if (hipGetLastError() != hipSuccess) {
+		if (sched)
+			sched_abort();
 		return -2;
+	}
 	if (sched)
 		sched_sampled(sched, d_counters, stream);
 	return 0;

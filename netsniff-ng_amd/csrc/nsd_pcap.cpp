@@ -914,6 +914,8 @@ struct ReplayStats {
 // So reading and walking batch k+1 overlap the rendering of batch k and the
 // writing of batch k-1.  A record above NSD_MAX_CAPLEN waits for everything
 // before it to be written, then goes through the per-packet path.
+extern "C" __attribute__((visibility("hidden"))) void nsd_if_cache_reset(void);   // nsd_format.cpp
+
 extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_prog *filter, int out_fd,
 				    int cols, uint64_t *counters, int threads, int pcap_fd)
 {
@@ -926,6 +928,7 @@ extern "C" long nsd_replay_pcap_out(const char *path, int mode, const nsd_bpf_pr
 	nsd_pcap *p = nsd_pcap_open(path);
 	if (!p)
 		return NSD_ERR_ARG;
+	nsd_if_cache_reset();   // interface names as they are now (renames since an earlier replay)
 	const int lt = (int)p->linktype;
 	// the dissector's SLL head reads the sockaddr_ll: an *_LL file's cooked
 	// headers, or a Kuznetzov / Borkmann file of an SLL link type (the frame

@@ -50,6 +50,7 @@ int render_packet_cpu(std::string &text, const uint8_t *packet, size_t len, int 
 
 extern "C" __attribute__((visibility("hidden"))) void nsd_device_ctx_release(void);
 extern "C" __attribute__((visibility("hidden"))) void nsd_replay_release(void);
+extern "C" __attribute__((visibility("hidden"))) void nsd_if_cache_reset(void);
 
 #ifndef NSD_ETCDIRE
 #define NSD_ETCDIRE "/etc/netsniff-ng"
@@ -417,6 +418,7 @@ extern "C" void dissector_cleanup_all(void)
 		dissector_cleanup_netlink();
 	nsd_device_ctx_release();
 	nsd_replay_release();
+	nsd_if_cache_reset();
 }
 
 // dissector.c:43-62

@@ -93,8 +93,11 @@ def max_over_ranks(values, device, group=None):
 def count_devices():
     """GPUs visible, counted in a child process so the caller initialises
     no GPU runtime before it spawns its ranks (0 if the count fails)."""
-    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
-                       stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=300)
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=300)
+    except (subprocess.TimeoutExpired, OSError):
+        return 0
     try:
         return int(r.stdout.strip().splitlines()[-1])
     except (ValueError, IndexError):

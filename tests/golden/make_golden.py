@@ -16,7 +16,11 @@
   prefix.json          SHA-256 of the nsref text of the first 65536 packets of
                        C2/C3/C4 (NORM, LESS) and of the oracle records / counters
   wsum.json            sum of W(pkt) (algorithmic read bytes) over
-                       the 16M-packet shards used by bench.py
+                       the 16M-packet shards used by bench.py (rank r of
+                       --gpus N walks shard r; 8 IMIX shards = C5)
+  shard_counters.json  the oracle's PRINT_NORM counter vector per bench shard
+                       (bench.py checks the all-reduced device counters
+                       against their sum; --shards-only: these two only)
   ip_vectors.npz       tests/ip_vectors.py: IPv4 / IPv6 / ICMPv4 frames and
                        the values the reference's csum.h / ipv4.h / ipv6.h
                        give for them (oracle/_ref/libnsdrefip.so; --ip-only)
@@ -140,6 +144,9 @@ def frame_goldens():
 
 def main():
     T.build_native()
+    if "--shards-only" in sys.argv:
+        wsum_shards()
+        return
     if "--fh-only" in sys.argv:
         frame_goldens()
         return
@@ -202,19 +209,28 @@ def prefix_digests():
 
 
 def wsum_shards():
-    wsum = {}
+    """wsum.json (ΣW per bench shard) and shard_counters.json (the oracle's
+    PRINT_NORM counter vector per bench shard): the 16M-packet shards
+    [r * 16M, (r + 1) * 16M) that rank r of `bench.py --gpus N` walks, r < 8,
+    for every bench config (8 IMIX shards = C5)."""
+    wsum, cnts = {}, {}
     n = 1 << 24
-    for key, cfg, shards in (("imix", T.SYN_IMIX, 8), ("ipv6x", T.SYN_IPV6X, 1)):
+    for key, cfg, shards in (("imix", T.SYN_IMIX, 8), ("ipv6x", T.SYN_IPV6X, 8), ("udp64", T.SYN_UDP64, 8)):
         for r in range(shards):
             frames, desc = T.make_batch(cfg, n, lo=r * n)
             counters = np.zeros(64, dtype=np.uint64)
             sw = T.oracle().nsor_dissect_batch_mt(frames.ctypes.data, desc.ctypes.data, n, 1,
                                                   T.PRINT_NORM, None, counters.ctypes.data, 8)
-            wsum[f"{key}:{r * n}:{n}"] = int(sw)
+            if key != "udp64":   # C2's W is caplen (bench.wsum_for)
+                wsum[f"{key}:{r * n}:{n}"] = int(sw)
+            cnts[f"{key}:{r * n}:{n}"] = [int(x) for x in counters]
             del frames, desc
             print(key, r, sw, flush=True)
     with open(os.path.join(HERE, "wsum.json"), "w") as f:
         json.dump(wsum, f, indent=1)
+    with open(os.path.join(HERE, "shard_counters.json"), "w") as f:
+        json.dump(cnts, f)
+
 
 
 if __name__ == "__main__":

@@ -54,6 +54,55 @@ def test_bench_rank_body(tmp_path):
         assert int(got[32]) == world * per_rank * steps
 
 
+def _run_worker(rank, world, port, per_rank, steps, out):
+    """One rank of bench.run (the N-rank output path of `bench.py --gpus N`)
+    with the host engine: the headline C2 and the C3 / C4 legs, each walked
+    by measure_rank and all-reduced; rank 0 saves the JSON line."""
+    import json
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"], os.environ["WORLD_SIZE"], os.environ["LOCAL_RANK"] = str(rank), str(world), str(rank)
+    sys.path.insert(0, ROOT)
+    import bench
+    nsd_dist.init("gloo")
+    r, w, _ = nsd_dist.rank_env()
+    args = bench.parse_args(["--gpus", str(w), "--packets", str(per_rank), "--steps", str(steps), "--warmup", "1"])
+    line = bench.run(args, r, w, "cpu", engine="host")
+    assert (line is None) == (r != 0)
+    if r == 0:
+        with open(out, "w") as f:
+            json.dump(line, f)
+    dist.destroy_process_group()
+
+
+def test_bench_line_n_ranks(tmp_path):
+    """`bench.py --gpus 2`'s line carries both north_star workloads (64 B C2
+    headline, IMIX leg: C5's layout at 8 ranks) and C4, each measured at
+    this N with its counters all-reduced over the ranks; the counters equal
+    the oracle's over both ranks' shards x the steps."""
+    import json
+    import bench
+    import nsd
+    world, per_rank, steps = 2, 4000, 2
+    out = str(tmp_path / "line.json")
+    mp.spawn(_run_worker, args=(world, nsd_dist.free_port(), per_rank, steps, out), nprocs=world, join=True)
+    with open(out) as f:
+        line = json.load(f)
+    assert line["n_gpus"] == world and line["scaling"] == "weak" and line["config"]["parallelism"] == "dp2"
+    assert set(line["legs"]) == {"imix", "ipv6x"}
+    assert "IMIX" in line["legs"]["imix"]["workload"] and "sharded across 2 GPUs" in line["legs"]["imix"]["workload"]
+    frames, desc = T.make_batch(T.SYN_UDP64, world * per_rank)
+    _, _, want, _ = T.oracle_records(frames, desc)
+    assert line["counters_total"] == world * per_rank * steps
+    for key, cfg in (("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):
+        leg = line["legs"][key]
+        assert leg["packets"] == world * per_rank and leg["value"] > 0
+        frames, desc = T.make_batch(cfg, world * per_rank)
+        _, _, want, _ = T.oracle_records(frames, desc)
+        assert leg["counters"] == nsd.unpack_counters(want * np.uint64(steps)), key
+    assert bench.golden_counters("imix", 1 << 24, 8) is not None   # the C5 shards are in the table
+
+
 def _dev_worker(rank, world, port, key, per_rank, steps, out):
     """One rank of the device branch: both ranks on cuda:0 (one GPU box),
     gloo over CUDA tensors (RCCL refuses two ranks on one device)."""
