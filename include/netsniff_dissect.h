@@ -454,6 +454,10 @@ long nsd_format_batch_compact(const uint8_t *frames, const nsd_desc_t *desc, con
 #define NSD_SCHED_FUSED    2
 int nsd_set_schedule(int sched);
 int nsd_last_schedule(void);
+/* nsd_set_grid_cap caps every batch walk's grid at `blocks` blocks (0: none,
+ * the default; tests use it to give small batches several tiles per wave).
+ * Process-wide; returns the previous cap, or NSD_ERR_ARG. */
+int nsd_set_grid_cap(int blocks);
 
 /* Compact-record pipe: nsd_pipe_create_compact as nsd_pipe_create, its
  * batches walked into nsd_crec records.  The pool needs ext_words >=

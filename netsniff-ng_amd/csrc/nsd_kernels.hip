@@ -470,6 +470,60 @@ __device__ __forceinline__ void put_rec(void *rec, uint32_t i, const WalkOut &w)
 	}
 }
 
+// The fused tile loop's compact records and pending-list entries, held one
+// tile (the 16-byte form stores at once: held, they spill registers): a
+// tile's stores are issued after the next tile's chunk wait and before its
+// prefetch loads, so the wait that precedes each tile (vmcnt(0): its chunks
+// are the youngest loads, and hipcc counts stores as pending vector-memory
+// operations too) never waits for a store just issued.  Issued at the end of
+// the tile instead, every tile's chunk wait also waited out its record
+// stores' round trip (C3 tile phase 0.348 -> 0.276 ms with the stores
+// removed altogether).
+template <bool CR>
+struct HeldSt {
+	uint2 r;          // the compact record (nsd_crec; 16-byte records are not held)
+	uint32_t ri;      // packet index of the record; ~0: none
+	uint64_t pe;      // pending-list entry
+	uint32_t pp;      // its slot; ~0: none
+	__device__ __forceinline__ void hold_rec(void *rec, uint32_t i, const WalkOut &w, bool on)
+	{
+		if constexpr (!CR) {
+			// (the 16-byte record is stored at once: held, its four words
+			// spill the fused kernel's registers)
+			if (on)
+				store_rec((uint4 *)rec, i, pack_record(w));
+			return;
+		}
+		ri = on ? i : 0xFFFFFFFFu;
+		if constexpr (CR) {
+			const bool more = w.n > NSD_REC_MAX_LAYERS;
+			const uint32_t nf = (more ? NSD_N_EXT : w.n) | w.flags;
+			const uint32_t rs = more && !w.ext_on ? w.n : 0u;
+			r = make_uint2(w.ext_on ? w.slot : w.chain, w.ip_csum | nf << 16 | rs << 24);
+		}
+	}
+	__device__ __forceinline__ void hold_pend(uint64_t *wq, uint64_t e, uint32_t slot)
+	{
+		if constexpr (!CR) {
+			if (slot != 0xFFFFFFFFu)
+				wq[slot] = e;   // (not held either, as the 16-byte record)
+			return;
+		}
+		pe = e;
+		pp = slot;
+	}
+	__device__ __forceinline__ void flush(void *rec, uint64_t *wq)
+	{
+		if constexpr (!CR)
+			return;
+		if (ri != 0xFFFFFFFFu)
+			__builtin_nontemporal_store(v2u{ r.x, r.y }, (v2u *)rec + ri);
+		if (pp != 0xFFFFFFFFu)
+			wq[pp] = pe;
+		ri = pp = 0xFFFFFFFFu;
+	}
+};
+
 // The split fast loop's stores.  With NSD_FAST_ASMST they are inline-asm
 // vector stores: hipcc's waitcnt pass treats the vector-memory counter as
 // out of order while loads and stores are both pending and then waits
@@ -897,208 +951,135 @@ __device__ __forceinline__ void take(Shared &sh, Walker &wk, bool &pnd, const Wa
 	pnd = pnd && rp >= nf;
 }
 
-// ---- the walk ------------------------------------------------------------------
-// Every packet of the block's grid-stride tiles, one wave per 64-packet tile:
-// the fast walk over each packet's first 64 bytes, then the general walk's
-// walkers take the packets it could not finish (walkers); ICMPv4 messages
-// past the windows and host-rendered leaves go to the wave's pending list
-// (pq).
-template <int MODE, bool CR>
-__device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict__ frames,
-					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
-					   void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
-					   uint32_t *__restrict__ ext_used, uint32_t chunk,
-					   const uint32_t *__restrict__ sll, Pending &pq,
-					   unsigned long long *__restrict__ sched)
+// plain_walk / plain4_walk map protocols 1 / 6 / 17 without the eth_lay3
+// lookup fast_walk makes: the table must agree
+constexpr uint8_t k_plain_lay3[256] = NSD_LAY3_TABLE;
+
+// The IMIX chains (PRINT_NORM, both schedules): Ethernet, at most one
+// 802.1Q tag, IPv4 without options, then TCP, UDP or ICMPv4, in a frame of
+// at least 38 bytes (every pull up to the IPv4 header succeeds and the header
+// lies in the window).  For such a packet fast_walk reads the tag, the IPv4
+// header, the total length (trim), the protocol and - for ICMPv4 - the
+// message (proto_icmpv4.c:34-51: whole post-trim message summed, inside the
+// window, or left to the checksum pass), and the chain ends after the L4
+// ops.  plain4_is / plain4_walk do the same from 9 row dwords read at once
+// (bytes 12..43 by byte funnel shifts, one LDS wait) instead of fast_walk's
+// chain of dependent byte reads and lookups; a tile takes this path when
+// every valid lane's packet qualifies (wave-uniform), and its per-ops counts
+// come from ballots.  The tag, ICMPv4 and TCP / UDP maps of eth_lay2 /
+// eth_lay3 are asserted below.
+#ifndef NSD_PLAIN4
+#define NSD_PLAIN4 0          // the fused kernel's tiles (r05: C3 within noise once its stores were held, C4 +2 %)
+#endif
+#ifndef NSD_PLAIN4_SPLIT
+#define NSD_PLAIN4_SPLIT 0    // the split fast kernel's tiles
+#endif
+static_assert(k_plain_lay3[1] == NSD_OPS_ICMPV4, "plain4_walk's protocol map differs from eth_lay3");
+struct Plain4 {
+	uint32_t E[6];   // bytes 12+v .. 35+v as little-endian dwords (v: the tag's 4 bytes, or 0)
+	bool vlan;
+};
+__device__ __forceinline__ Plain4 plain4_read(const LSrc<true, WIN1> &s)
 {
-	constexpr int ROW = row_of(WIN1);
-	auto &s_win = sh.win;
-	unsigned long long *const s_cnt = sh.cnt;
-	const uint8_t *const s_lay3 = sh.lay3;
-	const int lane = threadIdx.x & 63;
-	const int wv = threadIdx.x >> 6;
-
-	const uint32_t stride = gridDim.x * BLOCK;
-	uint64_t *const wq = pq.wq;
-	// compact records: pool words [0, n) are the packets' side words (when the
-	// pool has them), entries come after
-	const bool side = CR && ext_words >= n;
-	const GenSink<CR> g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.ops, &sh.lay[wv][0],
-			 side ? n : 0u, side ? ext : nullptr };
-	FlagCnt fc;
-	uint32_t ndefer = 0;
-	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
-
-	if (MODE != PRINT_NORM && MODE != PRINT_LESS) {
-		// every process() is NULL: no chain (dissector.c:51-53)
-		for (; base < n; base += stride) {
-			const uint32_t i = base + lane;
-			fc.pkts += FlagCnt::pc(i < n);
-			if (i < n) {
-				const uint32_t caplen = NSD_DESC_CAPLEN(desc[i]);
-				if constexpr (CR)
-					__builtin_nontemporal_store(v2u{ 0u, 0u }, (v2u *)rec + i);
-				else
-					store_rec((uint4 *)rec, i, make_uint4(0, caplen << 16, 0, 0));
-				fc.bytes += caplen;
+	const uint32_t r = s.m + 12, j = r >> 2, sh = r & 3;   // j + 8 <= 14: inside the row
+	uint32_t W[9], D[8];
+#pragma unroll
+	for (int k = 0; k < 9; k++)
+		W[k] = s.dw(j + k);
+#pragma unroll
+	for (int k = 0; k < 8; k++)
+		D[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
+	Plain4 p;
+	p.vlan = (D[0] & 0xFFFF) == 0x0081u;   // ethertype 0x8100 at byte 12
+#pragma unroll
+	for (int k = 0; k < 6; k++)
+		p.E[k] = p.vlan ? D[k + 1] : D[k];
+	return p;
+}
+// the ethertype at byte 12 alone: a first test that costs a tile of other
+// traffic (C4's IPv6) two row reads instead of plain4_read's nine
+__device__ __forceinline__ bool plain4_may(const LSrc<true, WIN1> &s)
+{
+	const uint32_t r = s.m + 12, j = r >> 2;
+	const uint32_t t = __builtin_amdgcn_alignbyte(s.dw(j + 1), s.dw(j), r & 3) & 0xFFFF;
+	return t == 0x0008u || t == 0x0081u;
+}
+__device__ __forceinline__ bool plain4_ok(const Plain4 &p, uint32_t caplen)
+{
+	// type 0x0800 at 12 + v (the inner type behind a tag), version / IHL 0x45,
+	// protocol 1 / 6 / 17
+	const uint32_t proto = p.E[2] >> 24;
+	return caplen >= 38 && (p.E[0] & 0xFFFFFFu) == 0x450008u && (proto == 1 || proto == 6 || proto == 17);
+}
+template <bool FOLD>
+__device__ __forceinline__ void plain4_walk(const LSrc<true, WIN1> &s, const Plain4 &p, uint32_t caplen, WalkOut &w)
+{
+	const uint32_t v = p.vlan ? 4u : 0u;
+	const uint32_t d2 = 34 + v;   // the L4 header
+	// calc_csum over the 10 header words at 14 + v (csum.h:12-27)
+	uint32_t sum = (p.E[0] >> 16) + (p.E[5] & 0xFFFF);
+#pragma unroll
+	for (int k = 1; k < 5; k++)
+		sum = __builtin_amdgcn_sad_u16(p.E[k], 0u, sum);
+	sum = (sum >> 16) + (sum & 0xffff);
+	sum += sum >> 16;
+	w.ip_csum = (uint16_t)~sum;
+	// the total-length trim (proto_ipv4.c:170-177; ihl 5)
+	const int32_t x = (int32_t)__builtin_bswap16((uint16_t)p.E[1]) - 20;
+	if (x >= 0 && (uint32_t)x < caplen - d2)
+		w.tail = d2 + (uint32_t)x;
+	const uint32_t proto = p.E[2] >> 24;
+	const int l4 = proto == 6 ? NSD_OPS_TCP : proto == 17 ? NSD_OPS_UDP : NSD_OPS_ICMPV4;
+	w.chain = p.vlan ? NSD_OPS_ETHERNET | NSD_OPS_VLAN << 5 | NSD_OPS_IPV4 << 10 | (uint32_t)l4 << 15
+			 : NSD_OPS_ETHERNET | NSD_OPS_IPV4 << 5 | (uint32_t)l4 << 10;
+	w.offA = p.vlan ? (uint64_t)14 << 16 | (uint64_t)18 << 32 | (uint64_t)38 << 48
+			: (uint64_t)14 << 16 | (uint64_t)34 << 32;
+	w.n = p.vlan ? 4 : 3;
+	const uint32_t len = w.tail - d2, hl = proto == 6 ? 20u : 8u;
+	w.data = len >= hl ? d2 + hl : d2;
+	if (l4 == NSD_OPS_ICMPV4 && len >= 8) {
+		// proto_icmpv4.c:42: calc_csum(icmp, pkt_len + 8) over the message
+		if (!s.in_window(d2, len & ~1u)) {
+			w.icmp_pend = true;
+			w.icmp_off = d2;
+			w.icmp_len = len;
+			if (FOLD) {
+				const uint32_t kw = s.window_bytes(d2) >> 1;
+				w.icmp_sum = s.sum16(d2, kw);
+				w.icmp_off = d2 + 2 * kw;
+				w.icmp_len = (len & ~1u) - 2 * kw;
 			}
+		} else if (calc_csum(s, d2, len >> 1)) {
+			w.flags |= NSD_F_ICMP_BAD;
 		}
-		fc.flush(s_cnt, lane);
-		return;
 	}
-
-	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
-	// descriptors are in flight
-	if (base >= n)
-		return;
-	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
-	uint64_t d1 = (base + stride < n && base + stride + lane < n) ? desc[base + stride + lane] : 0;
-	Chunks<WIN1> ch;
-	stage_load<WIN1>(ch, frames, d0, lane);
-	Walker wk;
-	walk_init(wk.w, 0, 0);
-	wk.d = 0;
-	wk.i = 0;
-	wk.wb = 0;
-	wk.wl = 0;
-	wk.have = false;
-	wk.stage = false;
-
-	// late: the next tile's chunks load after this tile's walkers (this tile's
-	// predecessor was walker-heavy: NSD_LATE, below)
-	bool late = false;
-	// (one more pass after the last tile drains the walkers: the engine is
-	// inlined once)
-	for (;; base += stride) {
-		const bool last = base >= n;
-		const uint32_t i = base + lane;
-		const bool valid = i < n;
-		const uint64_t off = NSD_DESC_OFF(d0);
-		const uint32_t caplen = NSD_DESC_CAPLEN(d0);
-		WalkOut w;
-		walk_init(w, caplen, valid ? start_id : 0);
-		bool deferred = false;
-		uint64_t d2 = 0;
-		if (!last) {
-			stage_write(&s_win[wv][0], ch, lane);
-			// prefetch: descriptors of tile t+2, chunks of tile t+1
-			const uint32_t b2 = base + 2 * stride;
-			d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
-			const uint32_t b1 = base + stride;
-			if (b1 < n && !late)
-				stage_load<WIN1>(ch, frames, d1, lane);
-			wave_sync_lds();
-
-			uint32_t fw = FW_DONE;
-			if (valid) {
-				const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
-							    (uint32_t)off & 15, 0, false };
-				fw = fast_walk<MODE, false, NSD_FAST_EXT != 0>(src, caplen, w);
-			}
-			deferred = fw != FW_DONE;
-			ndefer += FlagCnt::pc(deferred);
-			wave_sync_lds();
-			const bool done = valid && !deferred;
-			if (MODE == PRINT_NORM) {
-				// ICMPv4 messages past the window: listed for the checksum pass, which
-				// patches the record if the sum is bad
-				const bool pnd = w.icmp_pend && done;
-				const uint64_t pmask = __ballot(pnd);
-				if (pnd)
-					wq[pq.npend + lanes_below(pmask)] = pend_entry(i, w.icmp_off, w.icmp_len);
-				pq.npend += (uint32_t)__popcll(pmask);
-			}
-			// per-ops counts from the finished chains, grouped by chain word
-			// (ids are >= 1, so equal chain words imply equal layer counts) for
-			// the first two distinct chains of the tile (C2: one), the rest per
-			// lane (C3: -4.5 % against looping over every distinct chain)
-			{
-				uint32_t key = done ? w.chain : 0xFFFFFFFFu;
-				for (int it = 0;; it++) {
-					const uint64_t pm = __ballot(key != 0xFFFFFFFFu);
-					if (!pm)
-						break;
-					if (it == 2) {
-						// more than two distinct chains in the tile: the rest
-						// count their own layers (the LDS serialises them)
-						if (key != 0xFFFFFFFFu)
-							for (uint32_t k = 0; k < w.n; k++)
-								atomicAdd(&sh.ops[(key >> (5 * k)) & 31], 1u);
-						break;
-					}
-					const int leader = __ffsll((unsigned long long)pm) - 1;
-					const uint32_t lk = __shfl(key, leader, 64);
-					const uint64_t m = __ballot(key == lk);
-					if (lane == leader) {
-						const uint32_t cnt = (uint32_t)__popcll(m);
-						for (uint32_t k = 0, nl = w.n; k < nl; k++)
-							atomicAdd(&sh.ops[(lk >> (5 * k)) & 31], cnt);
-					}
-					if (key == lk)
-						key = 0xFFFFFFFFu;
-				}
-			}
-			if (CR && g.side && done && (w.flags & NSD_F_HOST)) {
-				// a leaf the fast walk finished (ARP, DCCP): its end in the side word
-				g.side[i] = w.data;
-				w.flags |= NSD_F_LEAF_END;
-			}
-			if (done)
-				put_rec<CR>(rec, i, w);
-			fc.add(w, caplen, done);
-			// the deferred packets' walk state for the general walk: from the
-			// start (FW_RESTART: other link types, MPLS, deeper tag stacks, bytes
-			// past the first window) or from where the fast walk stopped
-			// (FW_RESUME: its layers recorded; its finished chains are counted by
-			// chain word, these are counted here)
-			if (deferred) {
-				if (fw == FW_RESTART) {
-					walk_init(w, caplen, start_id);
-					if (start_id == NSD_OPS_SLL)
-						sll_head<MODE>(sh, w, sll, i);
-				} else {
-					for (uint32_t k = 0; k < w.n; k++)
-						atomicAdd(&sh.ops[(w.chain >> (5 * k)) & 31], 1u);
-				}
-			}
-		}
-		// (the walkers carried over are suspended: their windows are
-		// restaged anyway, so this tile's staging may reuse their rows)
-		bool pnd = deferred;
-		const bool many = __popcll(__ballot(pnd)) >= NSD_L2PF;
-		if (__ballot(pnd || wk.have))
-			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, pnd, w, i, d0, last);
-		if (last)
-			break;
-		// After a walker-heavy tile (C4) the next tile's chunks load here, with
-		// L2-allocating loads, rather than a tile ahead: its walkers' first
-		// windows then find the packets' first lines in L2 (loaded a tile
-		// ahead, those lines had left L2 by the time the walkers staged them:
-		// C4 400 -> 349 B/packet, 1.152 -> 1.107 ms on one box).  The chunk
-		// registers are dead during the walkers either way.
-		if (late && base + stride < n)
-			stage_load<WIN1, false, false>(ch, frames, d1, lane);
-		// (NSD_LATE 0: the chunks load a tile ahead, and while the walkers are
-		// busy the lines of tile t+2 go into L2 now, so the next iteration's
-		// loads of them wait for L2 rather than HBM: C4 1.45 -> 1.32 ms then.
-		// Not for tiles the fast walk finishes (C2, C3): there the next loads
-		// would wait for the touches (vector memory counts in order; C2
-		// +12 %).  The LDS-DMA target is window words past the fast rows.)
-		{
-			const uint32_t b2 = base + 2 * stride;
-			if (!NSD_LATE && many && b2 < n)
-				l2_touch(frames, d2, &s_win[wv][64 * ROW], b2 + lane < n);
-		}
-		late = NSD_LATE && many;
-		d0 = d1;
-		d1 = d2;
+}
+// a plain4 tile's per-ops counts and flag counts from ballots (no host leaf,
+// ext chain, overflow or deferral in such a tile)
+__device__ __forceinline__ void plain4_count(uint32_t *s_ops, FlagCnt &fc, const WalkOut &w, bool valid,
+					     uint32_t caplen, int lane)
+{
+	const int l4 = (int)((w.chain >> (w.n == 4 ? 15 : 10)) & 31);
+	const uint32_t nv = FlagCnt::pc(valid), ng = FlagCnt::pc(valid && w.n == 4);
+	const uint32_t nt = FlagCnt::pc(valid && l4 == NSD_OPS_TCP), nu = FlagCnt::pc(valid && l4 == NSD_OPS_UDP);
+	if (lane == 0) {
+		atomicAdd(&s_ops[NSD_OPS_ETHERNET], nv);
+		atomicAdd(&s_ops[NSD_OPS_IPV4], nv);
+		if (ng)
+			atomicAdd(&s_ops[NSD_OPS_VLAN], ng);
+		if (nt)
+			atomicAdd(&s_ops[NSD_OPS_TCP], nt);
+		if (nu)
+			atomicAdd(&s_ops[NSD_OPS_UDP], nu);
+		if (nv - nt - nu)
+			atomicAdd(&s_ops[NSD_OPS_ICMPV4], nv - nt - nu);
 	}
-	fc.flush(s_cnt, lane);
-	// the schedule sample (a launch the launcher samples passes its pair)
-	if (sched && lane == 0 && ndefer)
-		atomicAdd(&sched[0], (unsigned long long)ndefer);
-	if (sched && lane == 0 && pq.npend)
-		atomicAdd(&sched[1], (unsigned long long)pq.npend);
+	fc.pkts += nv;
+	fc.ipbad += FlagCnt::pc(valid && w.ip_csum != 0);
+	fc.icmpbad += FlagCnt::pc(valid && (w.flags & NSD_F_ICMP_BAD));
+	fc.trim += FlagCnt::pc(valid && w.tail < caplen);
+	if (valid)
+		fc.bytes += caplen;
 }
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
@@ -1177,6 +1158,230 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 	}
 	if (lane == 0 && bad)
 		atomicAdd(&sh.cnt[NSD_CNT_ICMP_BAD], (unsigned long long)bad);
+}
+
+// ---- the walk ------------------------------------------------------------------
+// Every packet of the block's grid-stride tiles, one wave per 64-packet tile:
+// the fast walk over each packet's first 64 bytes, then the general walk's
+// walkers take the packets it could not finish (walkers); ICMPv4 messages
+// past the windows and host-rendered leaves go to the wave's pending list
+// (pq).
+template <int MODE, bool CR>
+__device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict__ frames,
+					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
+					   void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
+					   uint32_t *__restrict__ ext_used, uint32_t chunk,
+					   const uint32_t *__restrict__ sll, Pending &pq,
+					   unsigned long long *__restrict__ sched)
+{
+	constexpr int ROW = row_of(WIN1);
+	auto &s_win = sh.win;
+	unsigned long long *const s_cnt = sh.cnt;
+	const uint8_t *const s_lay3 = sh.lay3;
+	const int lane = threadIdx.x & 63;
+	const int wv = threadIdx.x >> 6;
+
+	const uint32_t stride = gridDim.x * BLOCK;
+	uint64_t *const wq = pq.wq;
+	// compact records: pool words [0, n) are the packets' side words (when the
+	// pool has them), entries come after
+	const bool side = CR && ext_words >= n;
+	const GenSink<CR> g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.ops, &sh.lay[wv][0],
+			 side ? n : 0u, side ? ext : nullptr };
+	FlagCnt fc;
+	uint32_t ndefer = 0;
+	uint32_t base = blockIdx.x * BLOCK + wv * 64;   // this wave's tile; whole waves iterate
+
+	if (MODE != PRINT_NORM && MODE != PRINT_LESS) {
+		// every process() is NULL: no chain (dissector.c:51-53)
+		for (; base < n; base += stride) {
+			const uint32_t i = base + lane;
+			fc.pkts += FlagCnt::pc(i < n);
+			if (i < n) {
+				const uint32_t caplen = NSD_DESC_CAPLEN(desc[i]);
+				if constexpr (CR)
+					__builtin_nontemporal_store(v2u{ 0u, 0u }, (v2u *)rec + i);
+				else
+					store_rec((uint4 *)rec, i, make_uint4(0, caplen << 16, 0, 0));
+				fc.bytes += caplen;
+			}
+		}
+		fc.flush(s_cnt, lane);
+		return;
+	}
+
+	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
+	// descriptors are in flight
+	if (base >= n)
+		return;
+	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
+	uint64_t d1 = (base + stride < n && base + stride + lane < n) ? desc[base + stride + lane] : 0;
+	Chunks<WIN1> ch;
+	stage_load<WIN1>(ch, frames, d0, lane);
+	Walker wk;
+	walk_init(wk.w, 0, 0);
+	wk.d = 0;
+	wk.i = 0;
+	wk.wb = 0;
+	wk.wl = 0;
+	wk.have = false;
+	wk.stage = false;
+
+	// late: the next tile's chunks load after this tile's walkers (this tile's
+	// predecessor was walker-heavy: NSD_LATE, below)
+	bool late = false;
+	HeldSt<CR> hs;   // the previous tile's record / pending-list stores
+	hs.ri = hs.pp = 0xFFFFFFFFu;
+	// (one more pass after the last tile drains the walkers: the engine is
+	// inlined once)
+	for (;; base += stride) {
+		const bool last = base >= n;
+		const uint32_t i = base + lane;
+		const bool valid = i < n;
+		const uint64_t off = NSD_DESC_OFF(d0);
+		const uint32_t caplen = NSD_DESC_CAPLEN(d0);
+		WalkOut w;
+		walk_init(w, caplen, valid ? start_id : 0);
+		bool deferred = false;
+		uint64_t d2 = 0;
+		if (!last) {
+			stage_write(&s_win[wv][0], ch, lane);
+			hs.flush(rec, wq);   // tile t-1's stores, before tile t+1's loads
+			// prefetch: descriptors of tile t+2, chunks of tile t+1
+			const uint32_t b2 = base + 2 * stride;
+			d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
+			const uint32_t b1 = base + stride;
+			if (b1 < n && !late)
+				stage_load<WIN1>(ch, frames, d1, lane);
+			wave_sync_lds();
+
+			uint32_t fw = FW_DONE;
+			const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
+						    (uint32_t)off & 15, 0, false };
+			// a tile of IMIX chains only: the straight-line walk (plain4_walk)
+			bool p4 = false;
+			if (NSD_PLAIN4 && MODE == PRINT_NORM && start_id == NSD_OPS_ETHERNET &&
+			    __ballot(valid && !plain4_may(src)) == 0) {
+				const Plain4 pr = plain4_read(src);
+				p4 = __ballot(valid && !plain4_ok(pr, caplen)) == 0;
+				if (p4 && valid)
+					plain4_walk<false>(src, pr, caplen, w);
+			}
+			if (!p4 && valid)
+				fw = fast_walk<MODE, false, NSD_FAST_EXT != 0>(src, caplen, w);
+			deferred = fw != FW_DONE;
+			ndefer += FlagCnt::pc(deferred);
+			wave_sync_lds();
+			const bool done = valid && !deferred;
+			if (MODE == PRINT_NORM) {
+				// ICMPv4 messages past the window: listed for the checksum pass, which
+				// patches the record if the sum is bad
+				const bool pnd = w.icmp_pend && done;
+				const uint64_t pmask = __ballot(pnd);
+				hs.hold_pend(wq, pend_entry(i, w.icmp_off, w.icmp_len),
+					     pnd ? pq.npend + lanes_below(pmask) : 0xFFFFFFFFu);
+				pq.npend += (uint32_t)__popcll(pmask);
+			}
+			// per-ops counts from the finished chains, grouped by chain word
+			// (ids are >= 1, so equal chain words imply equal layer counts) for
+			// the first two distinct chains of the tile (C2: one), the rest per
+			// lane (C3: -4.5 % against looping over every distinct chain); a
+			// plain4 tile's from ballots
+			if (p4) {
+				plain4_count(sh.ops, fc, w, valid, caplen, lane);
+				hs.hold_rec(rec, i, w, valid);
+			} else {
+				uint32_t key = done ? w.chain : 0xFFFFFFFFu;
+				for (int it = 0;; it++) {
+					const uint64_t pm = __ballot(key != 0xFFFFFFFFu);
+					if (!pm)
+						break;
+					if (it == 2) {
+						// more than two distinct chains in the tile: the rest
+						// count their own layers (the LDS serialises them)
+						if (key != 0xFFFFFFFFu)
+							for (uint32_t k = 0; k < w.n; k++)
+								atomicAdd(&sh.ops[(key >> (5 * k)) & 31], 1u);
+						break;
+					}
+					const int leader = __ffsll((unsigned long long)pm) - 1;
+					const uint32_t lk = __shfl(key, leader, 64);
+					const uint64_t m = __ballot(key == lk);
+					if (lane == leader) {
+						const uint32_t cnt = (uint32_t)__popcll(m);
+						for (uint32_t k = 0, nl = w.n; k < nl; k++)
+							atomicAdd(&sh.ops[(lk >> (5 * k)) & 31], cnt);
+					}
+					if (key == lk)
+						key = 0xFFFFFFFFu;
+				}
+			if (CR && g.side && done && (w.flags & NSD_F_HOST)) {
+				// a leaf the fast walk finished (ARP, DCCP): its end in the side word
+				g.side[i] = w.data;
+				w.flags |= NSD_F_LEAF_END;
+			}
+			hs.hold_rec(rec, i, w, done);
+			fc.add(w, caplen, done);
+			}
+			// the deferred packets' walk state for the general walk: from the
+			// start (FW_RESTART: other link types, MPLS, deeper tag stacks, bytes
+			// past the first window) or from where the fast walk stopped
+			// (FW_RESUME: its layers recorded; its finished chains are counted by
+			// chain word, these are counted here)
+			if (deferred) {
+				if (fw == FW_RESTART) {
+					walk_init(w, caplen, start_id);
+					if (start_id == NSD_OPS_SLL)
+						sll_head<MODE>(sh, w, sll, i);
+				} else {
+					for (uint32_t k = 0; k < w.n; k++)
+						atomicAdd(&sh.ops[(w.chain >> (5 * k)) & 31], 1u);
+				}
+			}
+		}
+		// (the walkers carried over are suspended: their windows are
+		// restaged anyway, so this tile's staging may reuse their rows)
+		bool pnd = deferred;
+		const bool many = __popcll(__ballot(pnd)) >= NSD_L2PF;
+		if (__ballot(pnd || wk.have)) {
+			// (the walkers wait for their windows anyway: the held stores go
+			// first, and nothing is held across the engine's registers)
+			hs.flush(rec, wq);
+			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, pnd, w, i, d0, last);
+		}
+		if (last) {
+			hs.flush(rec, wq);
+			break;
+		}
+		// After a walker-heavy tile (C4) the next tile's chunks load here, with
+		// L2-allocating loads, rather than a tile ahead: its walkers' first
+		// windows then find the packets' first lines in L2 (loaded a tile
+		// ahead, those lines had left L2 by the time the walkers staged them:
+		// C4 400 -> 349 B/packet, 1.152 -> 1.107 ms on one box).  The chunk
+		// registers are dead during the walkers either way.
+		if (late && base + stride < n)
+			stage_load<WIN1, false, false>(ch, frames, d1, lane);
+		// (NSD_LATE 0: the chunks load a tile ahead, and while the walkers are
+		// busy the lines of tile t+2 go into L2 now, so the next iteration's
+		// loads of them wait for L2 rather than HBM: C4 1.45 -> 1.32 ms then.
+		// Not for tiles the fast walk finishes (C2, C3): there the next loads
+		// would wait for the touches (vector memory counts in order; C2
+		// +12 %).  The LDS-DMA target is window words past the fast rows.)
+		{
+			const uint32_t b2 = base + 2 * stride;
+			if (!NSD_LATE && many && b2 < n)
+				l2_touch(frames, d2, &s_win[wv][64 * ROW], b2 + lane < n);
+		}
+		late = NSD_LATE && many;
+		d0 = d1;
+		d1 = d2;
+	}
+	fc.flush(s_cnt, lane);
+	// the schedule sample (a launch the launcher samples passes its pair)
+	if (sched && lane == 0 && ndefer)
+		atomicAdd(&sched[0], (unsigned long long)ndefer);
+	if (sched && lane == 0 && pq.npend)
+		atomicAdd(&sched[1], (unsigned long long)pq.npend);
 }
 
 // ---- host-rendered leaves -------------------------------------------------------
@@ -1361,7 +1566,6 @@ __device__ __forceinline__ uint32_t fold_weighted(uint32_t sum, bool odd)
 // (wave-uniform), so a mixed tile runs fast_walk alone.
 // plain_is / plain_walk map protocol 6 / 17 to TCP / UDP without the eth_lay3
 // lookup fast_walk makes: the table must agree
-constexpr uint8_t k_plain_lay3[256] = NSD_LAY3_TABLE;
 static_assert(k_plain_lay3[6] == NSD_OPS_TCP && k_plain_lay3[17] == NSD_OPS_UDP,
 	      "plain_walk's protocol map differs from eth_lay3");
 
@@ -1476,11 +1680,21 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 		// (every lane's row is staged, a lane past the batch from the clamped descriptor)
 		const bool plain = MODE == PRINT_NORM && start_id == NSD_OPS_ETHERNET &&
 				   __ballot(valid && !plain_is(src, caplen)) == 0;
+		bool p4 = false;
 		if (plain) {
 			if (valid)
 				plain_walk(src, caplen, w);
-		} else if (valid) {
-			fw = fast_walk<MODE, true>(src, caplen, w);
+		} else {
+			// a tile of IMIX chains only: the straight-line walk (plain4_walk)
+			if (NSD_PLAIN4_SPLIT && MODE == PRINT_NORM && start_id == NSD_OPS_ETHERNET &&
+			    __ballot(valid && !plain4_may(src)) == 0) {
+				const Plain4 pr = plain4_read(src);
+				p4 = __ballot(valid && !plain4_ok(pr, caplen)) == 0;
+				if (p4 && valid)
+					plain4_walk<true>(src, pr, caplen, w);
+			}
+			if (!p4 && valid)
+				fw = fast_walk<MODE, true>(src, caplen, w);
 		}
 		const bool deferred = fw != FW_DONE;
 		wave_sync_lds();
@@ -1521,7 +1735,13 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 			nicmp += (uint32_t)__popcll(pm);
 		}
 		// per-ops counts of the finished chains, grouped by chain word (as
-		// walk_tiles)
+		// walk_tiles); a plain4 tile's from ballots
+		if (p4) {
+			plain4_count(sh.ops, fc, w, valid, caplen, lane);
+			if (valid)
+				put_rec_st<CR>(rec, i, w);
+			return;
+		}
 		{
 			uint32_t key = done ? w.chain : 0xFFFFFFFFu;
 			for (int it = 0;; it++) {
@@ -1988,6 +2208,7 @@ struct Sched {
 Sched g_sched[MAX_DEV];
 std::mutex g_sched_mu;
 int g_sched_force = 0;   // 0 adaptive, NSD_SCHED_SPLIT, NSD_SCHED_FUSED
+std::atomic<int> g_grid_cap{ 0 };   // nsd_set_grid_cap
 
 int cur_dev()
 {
@@ -2091,6 +2312,13 @@ extern "C" int nsd_set_schedule(int sched)
 	return prev;
 }
 
+extern "C" int nsd_set_grid_cap(int blocks)
+{
+	if (blocks < 0)
+		return NSD_ERR_ARG;
+	return g_grid_cap.exchange(blocks);
+}
+
 extern "C" int nsd_last_schedule(void)
 {
 	std::lock_guard<std::mutex> g(g_sched_mu);
@@ -2175,6 +2403,8 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 		}
 		return occ;
 	};
+	if (grid <= 0)
+		grid = g_grid_cap.load(std::memory_order_relaxed);
 	unsigned long long *const pair = d_ws ? (unsigned long long *)((uint8_t *)d_ws + sched_pair_at(n)) : nullptr;
 	const Plan plan = sched_plan(n, mi != 2 ? pair : nullptr, d_counters, stream);
 	const int s_cus = plan.cus;

@@ -79,7 +79,7 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_dissect_device_compact", "nsd_format_batch_compact", "nsd_pipe_create_compact",
                "nsd_pipe_submit_compact", "nsd_format_range_compact", "nsd_set_schedule",
                "nsd_last_schedule", "nsd_format_frame_hdr", "nsd_format_range_compact_fh",
-               "nsd_pcap_read_batch_fh", "nsd_t3_block_desc_fh", "nsd_pcap_index"]
+               "nsd_pcap_read_batch_fh", "nsd_t3_block_desc_fh", "nsd_pcap_index", "nsd_set_grid_cap"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -239,6 +239,15 @@ def set_schedule(sched):
     rc = lib().nsd_set_schedule(sched)
     if rc < 0:
         raise ValueError(f"bad schedule {sched}")
+    return rc
+
+
+def set_grid_cap(blocks):
+    """Cap every batch walk's grid at `blocks` blocks (0: none); returns the
+    previous cap (nsd_set_grid_cap, tests)."""
+    rc = lib().nsd_set_grid_cap(blocks)
+    if rc < 0:
+        raise ValueError(f"bad grid cap {blocks}")
     return rc
 
 

@@ -24,12 +24,28 @@ def native_build():
     yield
 
 
+def _schedule(request):
+    import nsd
+    prev = nsd.set_schedule(nsd.SCHED_SPLIT if request.param == "split" else nsd.SCHED_FUSED)
+    if request.param == "fused_grid3":
+        nsd.set_grid_cap(3)
+    yield request.param
+    nsd.set_schedule(prev)
+    nsd.set_grid_cap(0)
+
+
 @pytest.fixture(params=["split", "fused"])
 def schedule(request):
     """Runs a parity test under both kernel schedules (nsd_set_schedule): the
     split fast + walker kernels and the fused kernel must each match the
     oracle; the library's adaptive choice is restored after."""
-    import nsd
-    prev = nsd.set_schedule(nsd.SCHED_SPLIT if request.param == "split" else nsd.SCHED_FUSED)
-    yield request.param
-    nsd.set_schedule(prev)
+    yield from _schedule(request)
+
+
+@pytest.fixture(params=["split", "fused", "fused_grid3"])
+def schedule_small(request):
+    """`schedule` for small batches, plus the fused kernel with its grid
+    capped at 3 blocks (nsd_set_grid_cap), so each wave walks many tiles:
+    walkers carried across tiles, the pending lists of many tiles, waves of
+    a block with unequal tile counts."""
+    yield from _schedule(request)

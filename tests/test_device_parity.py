@@ -7,7 +7,7 @@ import edge_cases
 import nsd
 import nsd_testlib as T
 
-pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("schedule")]
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("schedule_small")]
 
 MODES = [T.PRINT_NORM, T.PRINT_LESS, T.PRINT_HEX]
 
@@ -475,8 +475,93 @@ def test_plain_tiles_partial_and_mixed(mode):
     _check_compact(frames, desc, mode)
 
 
+def _imix_tiles(seed=11, n=64 * 48):
+    """Ethernet / [one 802.1Q tag] / IPv4 (no options) / TCP, UDP or ICMPv4
+    frames only, so whole tiles take the straight-line IMIX walk
+    (plain4_walk, both schedules): frame lengths 38 .. 1500, total lengths
+    below the header, inside the frame (trimmed) and past it, good and bad
+    header checksums, ICMPv4 messages inside the window and past it with
+    good and bad sums, odd and even lengths, L4 bodies shorter than their
+    headers."""
+    import random
+    rnd = random.Random(seed)
+    pkts = []
+    for k in range(n):
+        vlan = rnd.random() < 0.5
+        v = 4 if vlan else 0
+        cap = rnd.choice([38, 41, 42, 45, 46, 53, 58, 62, 63, 64, 64, 64, 65, 66, 77, 90, 128, 200, 576, 1500])
+        cap = max(cap, 34 + v)
+        proto = rnd.choice([1, 1, 6, 17])
+        r = rnd.random()
+        room = cap - 14 - v
+        totlen = (rnd.randrange(0, 20) if r < 0.1 else rnd.randrange(room, room + 30) if r < 0.3
+                  else rnd.randrange(20, room + 1))
+        hdr = bytearray([0x45, rnd.randrange(256)]) + totlen.to_bytes(2, "big") + \
+            bytes(rnd.randrange(256) for _ in range(4)) + bytes([rnd.randrange(256), proto, 0, 0]) + \
+            bytes(rnd.randrange(256) for _ in range(8))
+        s = sum(int.from_bytes(hdr[i:i + 2], "big") for i in range(0, 20, 2))
+        while s >> 16:
+            s = (s & 0xFFFF) + (s >> 16)
+        hdr[10:12] = ((~s & 0xFFFF) if rnd.random() < 0.7 else rnd.randrange(65536)).to_bytes(2, "big")
+        body = bytearray(rnd.randrange(256) for _ in range(cap - 34 - v))
+        if proto == 1 and rnd.random() < 0.6:
+            # a good ICMPv4 sum over the post-trim message (odd trailing byte dropped)
+            x = totlen - 20   # the trim (proto_ipv4.c:174-175)
+            mlen = x if 0 <= x < len(body) else len(body)
+            if mlen >= 4:
+                body[2:4] = b"\0\0"
+                w = mlen & ~1
+                s = sum(int.from_bytes(body[i:i + 2], "little") for i in range(0, w, 2))
+                while s >> 16:
+                    s = (s & 0xFFFF) + (s >> 16)
+                body[2:4] = (~s & 0xFFFF).to_bytes(2, "little")
+        eth = bytes(rnd.randrange(256) for _ in range(12))
+        eth += (b"\x81\x00" + rnd.randrange(65536).to_bytes(2, "big") + b"\x08\x00") if vlan else b"\x08\x00"
+        pkts.append(eth + bytes(hdr) + bytes(body))
+    return pkts
+
+
+def _not_imix(rnd, pkt):
+    """One frame the IMIX path must refuse: IHL 6, a second tag, protocol 2
+    (IGMP), a frame too short for the IPv4 header, a QinQ outer tag."""
+    kind = rnd.randrange(5)
+    v = 4 if pkt[12:14] == b"\x81\x00" else 0
+    if kind == 0:
+        ip = bytearray(pkt[14 + v:34 + v])
+        ip[0] = 0x46
+        return pkt[:14 + v] + bytes(ip) + b"\x01\x01\x01\x00" + pkt[34 + v:]
+    if kind == 1:
+        return pkt[:12] + b"\x81\x00\x00\x05\x81\x00\x00\x06" + pkt[12 + v:]
+    if kind == 2:
+        return pkt[:23 + v] + b"\x02" + pkt[24 + v:]
+    if kind == 3:
+        return pkt[:33 + v]
+    return pkt[:12] + b"\x88\xa8\x00\x07" + pkt[12 + v:]
+
+
+@pytest.mark.parametrize("align", [1, 2, 16])
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_imix_tiles(mode, align):
+    """Tiles of IMIX chains only (the straight-line plain4 walk in PRINT_NORM)
+    at odd and even alignments, a partial last tile, and tiles with one
+    frame the path must refuse: records of both forms and counters equal the
+    oracle's, under both schedules."""
+    import random
+    rnd = random.Random(31 + align)
+    pkts = _imix_tiles(seed=align, n=64 * 40 + 9)
+    frames, desc = T.batch_from_packets(pkts, align=align)
+    _check(frames, desc, mode)
+    _check_compact(frames, desc, mode)
+    for t in range(0, 40, 3):
+        k = 64 * t + rnd.randrange(64)
+        pkts[k] = _not_imix(rnd, pkts[k])
+    frames, desc = T.batch_from_packets(pkts, align=align)
+    _check(frames, desc, mode)
+    _check_compact(frames, desc, mode)
+
+
 @pytest.mark.parametrize("compact", [False, True])
-def test_graph_capture_and_replay(compact, schedule):
+def test_graph_capture_and_replay(compact, schedule_small):
     """nsd_dissect_device_ws / _compact captured into a HIP graph (torch.cuda
     graph on the launch stream): the walk of a fixed-size batch replayed
     over new frames in the same buffers gives the oracle's records and
