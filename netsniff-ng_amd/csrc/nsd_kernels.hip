@@ -474,11 +474,14 @@ __device__ __forceinline__ void put_rec(void *rec, uint32_t i, const WalkOut &w)
 // tile (the 16-byte form stores at once: held, they spill registers): a
 // tile's stores are issued after the next tile's chunk wait and before its
 // prefetch loads, so the wait that precedes each tile (vmcnt(0): its chunks
-// are the youngest loads, and hipcc counts stores as pending vector-memory
-// operations too) never waits for a store just issued.  Issued at the end of
-// the tile instead, every tile's chunk wait also waited out its record
-// stores' round trip (C3 tile phase 0.348 -> 0.276 ms with the stores
-// removed altogether).
+// are the youngest loads) finds them issued a whole tile earlier (C3 -1 %).
+// (Nontemporal stores: as sc1 stores, the split kernel's choice below, C3
+// ran 1.5 % slower.)
+// Measured on the C3 tile phase without its walk: the record
+// stores cost 0.07 of its 0.35 ms however they are issued - every tile or
+// every fourth in 4x larger pieces, 8 or 16 bytes per lane, held or not -
+// i.e. the writes' interleaving with the scattered window reads in HBM, not
+// a wait in this loop.
 template <bool CR>
 struct HeldSt {
 	uint2 r;          // the compact record (nsd_crec; 16-byte records are not held)
@@ -532,7 +535,11 @@ struct HeldSt {
 // waits count the loop's loads alone; loads complete in order among
 // themselves, so a wait that leaves N later loads outstanding still covers
 // the load it waits for, whatever the stores do.  Their completion is ours:
-// drain_stores() before anything reads what they wrote.  A store of more
+// drain_stores() before anything reads what they wrote.  The record stores
+// use the sc1 policy (written through, the line dropped from the XCD's L2;
+// MI355X_MICROARCH.md "stores of each flavour"): C2 0.2069 - 0.2092 ->
+// 0.2036 - 0.2049 ms against nontemporal stores on one box (records are read
+// by the host or another kernel, never by this wave again).  A store of more
 // than 8 bytes reads its data registers over two cycles, and hipcc's hazard
 // recognizer does not know an asm statement is such a store: the next VALU
 // could overwrite the data before it is read (gfx9's 12-dword store hazard;
@@ -575,11 +582,11 @@ __device__ __forceinline__ void put_rec_st(void *rec, uint32_t i, const WalkOut 
 		const uint32_t nf = (more ? NSD_N_EXT : w.n) | w.flags;
 		const uint32_t rs = more && !w.ext_on ? w.n : 0u;
 		const v2u v = { w.ext_on ? w.slot : w.chain, w.ip_csum | nf << 16 | rs << 24 };
-		asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"((v2u *)rec + i), "v"(v) : "memory");
+		asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"((v2u *)rec + i), "v"(v) : "memory");
 	} else {
 		const uint4 r = pack_record(w);
 		const v4u v = { r.x, r.y, r.z, r.w };
-		asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"((uint4 *)rec + i), "v"(v) : "memory");
+		asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"((uint4 *)rec + i), "v"(v) : "memory");
 	}
 }
 
