@@ -115,9 +115,10 @@ struct GenSink {
 	// a host-rendered leaf ends the chain: its pulls are walked once the
 	// lane's chain is done (emit_general), where fewer registers are live
 	template <int MODE, class Src>
-	__device__ __forceinline__ void leaf(const Src &, bool lw, WalkOut &w, int id, uint32_t) const
+	__device__ __forceinline__ uint32_t leaf(const Src &, bool lw, WalkOut &w, int id, uint32_t, uint32_t nd) const
 	{
 		w.leaf = lw ? id : w.leaf;
+		return nd;
 	}
 };
 
@@ -206,10 +207,9 @@ struct HostSink {
 			counters[NSD_CNT_OPS + id]++;
 	}
 	template <int MODE, class Src>
-	__host__ void leaf(const Src &s, bool lw, WalkOut &w, int id, uint32_t start) const
+	__host__ uint32_t leaf(const Src &s, bool lw, WalkOut &w, int id, uint32_t start, uint32_t nd) const
 	{
-		if (lw)
-			w.data = leaf_end<MODE>(s, id, start, w.tail);
+		return lw ? leaf_end<MODE>(s, id, start, w.tail) : nd;
 	}
 };
 
@@ -374,15 +374,14 @@ NSD_HD int sll_next(uint32_t hatype, uint32_t proto, int mode, uint32_t e2)
 // layer: record the ops (chain word / offsets, or the ext pool entry once
 // the chain needs the ext form), count it, advance the pkt_buff cursor
 // exactly as the reference parser does, look up the next ops.
+// `info0`: the ops' rule word s.step(w.id), when the caller has read it.
 template <int MODE, class Src, class Sink>
-NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
+NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g, uint32_t info0)
 {
 	const int id = act ? w.id : 0;
 	const uint32_t start = w.data;
 	const uint32_t k = w.n;
-	// the ops' rule word (read before the sink's stores, so the device walk's
-	// near_end() read of the same word serves it)
-	const uint32_t info = act ? s.step(w.id) : 0u;
+	const uint32_t info = act ? info0 : 0u;
 	// ---- record the layer: the first 6 in the record; more than 6, or a
 	// layer past byte 510, forces the ext form
 	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
@@ -429,12 +428,19 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 
 	// HBH / DestOpts: opt_len = T8 - 2 <= pkt_len after the 2-byte pull;
 	// Routing: data_len = T8 - 4 <= pkt_len after the 4-byte pull.  These,
-	// the fixed pulls and the leaves are the common case; the other kinds'
-	// rules run only when a lane of the wave is on such a layer (instruction
-	// issue bounds the general walk)
-	const bool t8ok = T8 <= len;
-	uint32_t adv = kind == K_T8 ? (t8ok ? T8 : minl) : fadv;
-	bool cont = (kind == K_CONT) | ((kind == K_T8) & t8ok);
+	// AH, the fixed pulls and the leaves are the common case; the other
+	// kinds' rules run only when a lane of the wave is on such a layer
+	// (instruction issue bounds the general walk)
+	// AH (proto_ip_authentication_hdr.c:26-69): hdr_len = plen*4 + 8,
+	// checked against pkt_len after the 12-byte pull (hdr_len + 12 <= len),
+	// the ICV pulled when hdr_len > 12: the same rule with b1*4 + 8 and the
+	// check offset by 12
+	const bool isah = kind == K_AH;
+	const bool var = (kind == K_T8) | isah;
+	const uint32_t VL = (b1 << (isah ? 2u : 3u)) + 8u;
+	const bool vok = VL + (isah ? 12u : 0u) <= len;
+	uint32_t adv = var ? (vok ? (VL > minl ? VL : minl) : minl) : fadv;
+	bool cont = (kind == K_CONT) | (var & vok);
 	bool host = kind == K_HOST;
 	const bool isv4 = act & (kind == K_IPV4);
 	uint32_t ihl = 0;
@@ -452,14 +458,6 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 			const bool trim = pulled & (x >= 0) & ((uint64_t)x < len - v4adv);
 			w.tail = trim ? start + v4adv + (uint32_t)x : w.tail;
 		}
-	}
-	const bool isah = act & (kind == K_AH);
-	if (isah) {
-		// AH: hdr_len = plen*4 + 8, checked after the 12-byte pull, ICV pulled
-		const uint32_t hl = b1 * 4u + 8u;
-		const bool ahok = hl <= len - 12;
-		adv = 12 + ((ahok & (hl > 12)) ? hl - 12 : 0);
-		cont = ahok;
 	}
 	const bool ismob = act & (kind == K_MOB);
 	if (ismob) {
@@ -490,13 +488,15 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 	}
 	host = host & pulled;
 	const bool upd = act & (kind != K_MPLS);
-	w.data = upd ? start + (pulled ? adv : 0u) : w.data;
-	w.id = upd ? ((pulled & cont) ? nx : 0) : w.id;
+	// the new cursor and ops are stored last, after every use of the old
+	// ones (start, id): the walkers' loop then carries them in place
+	uint32_t nd = start + ((upd & pulled) ? adv : 0u);
+	int nid = upd ? ((pulled & cont) ? nx : 0) : w.id;
 	w.flags |= (upd & host) ? NSD_F_HOST : 0;
 	// a host-rendered leaf: where its parser's pulls leave the cursor
 	// (nsd_leaf.h), so the exit op's dump starts from the record; the
 	// sink decides when (the device walks it after the chain, emit_general)
-	g.template leaf<MODE>(s, upd & host, w, id, start);
+	nd = g.template leaf<MODE>(s, upd & host, w, id, start, nd);
 	// ---- the rare heavy bodies
 	const bool v4 = upd && kind == K_IPV4 && pulled;
 	if (MODE == PRINT_NORM && v4) {
@@ -527,15 +527,22 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
 				d += 4; l -= 4;
 				if (sbit) break;
 			}
-			w.data = d;
+			nd = d;
 			int nxt = 0;
 			if (ok && l) {
 				const uint8_t nib = s.b(d) >> 4;   // mpls_uc_next_proto :23-47
 				nxt = nib == 4 ? NSD_OPS_IPV4 : nib == 6 ? NSD_OPS_IPV6 : 0;
 			}
-			w.id = nxt;
+			nid = nxt;
 		}
 	}
+	w.data = nd;
+	w.id = nid;
+}
+template <int MODE, class Src, class Sink>
+NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g)
+{
+	gen_step<MODE>(s, act, w, g, s.step(w.id));
 }
 
 // Straight-line walk for the common chains (pass 1): Ethernet, up to two

@@ -47,6 +47,8 @@ def child(args):
     import numpy as np
     import torch
     import nsd
+    if args.lib:
+        nsd.LIB_PATH = os.path.abspath(args.lib)
     torch.cuda.set_device(0)
     nsd.set_schedule(nsd.SCHED_FUSED)
     for k in (args.k1, args.k2):
@@ -81,12 +83,14 @@ def main():
     ap.add_argument("--k2", type=int, default=9)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--lib", default=None, help="a variant libnsdissect.so (tools/build_variant.sh)")
     args = ap.parse_args()
     if args.child:
         child(args)
         return
     base = [sys.executable, os.path.abspath(__file__), "--child", "--packets", str(args.packets), "--k1",
-            str(args.k1), "--k2", str(args.k2), "--reps", str(args.reps)]
+            str(args.k1), "--k2", str(args.k2), "--reps", str(args.reps)] + \
+        (["--lib", os.path.abspath(args.lib)] if args.lib else [])
     r = subprocess.run(base, stdout=subprocess.PIPE, text=True, check=True)
     timing = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     with tempfile.TemporaryDirectory(dir="/tmp") as d:
