@@ -125,20 +125,22 @@ struct LSrc {
 	__device__ __forceinline__ uint32_t step(int id) const { return stept[id & 31]; }
 	__device__ __forceinline__ uint32_t l2h(uint32_t h) const { return stept[32 + (h & 31)]; }
 	// bytes o .. o+3 (little-endian) from the window row: two dwords and a
-	// byte funnel shift; zero at offsets >= caplen.  Meaningful only for
-	// bytes inside the window (a near_end() budget covers them).
+	// byte funnel shift.  Meaningful only for bytes inside the window (a
+	// near_end() budget covers them).  FAST: zero at offsets >= caplen.  The
+	// continuation rows are not zeroed past caplen and this read does not
+	// mask them: it serves gen_step's layer bytes (B0, the next-ops key) only,
+	// every use of which is gated by the layer's first pull succeeding
+	// (pulled: the bytes it reads lie before tail <= caplen), so a byte past
+	// the frame never reaches a result (C4 -1.4 %: 6 VALU per read).
 	__device__ __forceinline__ uint32_t dword_at(uint32_t o) const
 	{
 		const uint32_t r = o + m - wb;
 		uint32_t j = r >> 2;
 		j = j > WIN / 4 - 1 ? WIN / 4 - 1 : j;
 		const uint32_t v = __builtin_amdgcn_alignbyte(dw(j + 1), dw(j), r & 3);
-		if constexpr (FAST) {
+		if constexpr (FAST)
 			return o >= caplen ? 0u : v;
-		} else {
-			const uint32_t left = o >= caplen ? 0u : caplen - o;
-			return left >= 4 ? v : v & ((1u << (8 * left)) - 1u);
-		}
+		return v;
 	}
 	__device__ __forceinline__ bool missed() const { return miss; }
 	__device__ __forceinline__ uint8_t b(uint32_t o) const

@@ -181,7 +181,8 @@ __device__ __forceinline__ void GenSink<CR>::take_deep(bool deep_first, WalkOut 
 {
 	if (__ballot(deep_first)) {
 		// room for every layer the record may hold (the chain's length is not
-		// known yet)
+		// known yet); the wave-uniform test leaves the entry test to here
+		deep_first = deep_first && !w.ext_on;
 		const uint32_t sb = ext_take(*this, deep_first, NSD_EXT_WORDS(NSD_EXT_MAX_LAYERS));
 		if (deep_first) {
 			w.slot = sb;
@@ -386,7 +387,7 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g, uint32_t
 	// layer past byte 510, forces the ext form
 	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
 	const bool need_now = act && (k >= NSD_REC_MAX_LAYERS || (k >= 1 && start > 510));
-	g.take_deep(act && k == DEEP && !w.ext_on, w);
+	g.take_deep(act && k == DEEP, w);   // (entry taken unless ext_on)
 	const uint32_t kk = k < 8 ? k : 7;   // keeps the shifts below defined
 	w.need_ext = w.need_ext || need_now;
 	w.chain |= act && k < NSD_REC_MAX_LAYERS ? (uint32_t)id << (5 * kk) : 0u;
@@ -402,7 +403,9 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g, uint32_t
 		g.layer(w, k, id, start);
 	w.n = act ? k + 1 : k;
 
-	// ---- parse (bytes >= caplen read as zero).  The common rules are
+	// ---- parse.  Every use of the layer's bytes (B0, KD) is gated by the
+	// first pull (pulled), so bytes past the frame, which the device's
+	// continuation rows do not mask, never reach a result.  The common rules are
 	// computed for every lane and selected by the rule kind (boolean terms
 	// combined with & and | so the compiler keeps them as selects).
 	const uint32_t len = w.tail - start;   // pkt_len (pkt_buff.h:36-41)
