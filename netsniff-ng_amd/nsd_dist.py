@@ -58,10 +58,18 @@ def initialized():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def _grouped():
+    """A process group exists (a launch of any world size, one rank included:
+    its collectives then run through RCCL / gloo all the same); a plain
+    single-process run has none and skips them."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def reduce_counters(counters, group=None):
     """Sum the counter vectors of all ranks in place (int64 tensor)."""
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _grouped():
         dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
     return counters
 
@@ -70,14 +78,14 @@ def all_ranks_agree(flag, device, group=None):
     """True iff `flag` holds on every rank (MIN all-reduce of 0/1)."""
     import torch.distributed as dist
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _grouped():
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return bool(t.item())
 
 
 def barrier(group=None):
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _grouped():
         dist.barrier(group=group)
 
 
@@ -85,7 +93,7 @@ def max_over_ranks(values, device, group=None):
     """Max of a list of floats over ranks (bench timing)."""
     import torch.distributed as dist
     t = torch.tensor(values, dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _grouped():
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return [float(x) for x in t]
 

@@ -159,3 +159,61 @@ def test_shards_partition_exactly():
             assert rngs[0][0] == 0 and rngs[-1][1] == total
             assert all(a[1] == b[0] for a, b in zip(rngs, rngs[1:]))
     assert nsd_dist.weak_shard(16, 3) == (48, 64)
+
+
+def _nccl_worker(rank, world, port, per_rank, steps, out):
+    """bench.run under an RCCL process group of one rank on cuda:0 (a
+    one-GPU box cannot hold two RCCL ranks): nsd_dist.init("nccl") binds
+    the device, and the counter all-reduce, the agreement MIN, the barrier
+    and the MAX of the times go through RCCL on device tensors."""
+    import json
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"], os.environ["WORLD_SIZE"], os.environ["LOCAL_RANK"] = str(rank), str(world), str(rank)
+    sys.path.insert(0, ROOT)
+    import bench
+    nsd_dist.init("nccl", 0)
+    calls = []
+    real = dist.all_reduce
+
+    def counted(t, *a, **k):
+        calls.append(t.device.type)
+        return real(t, *a, **k)
+    dist.all_reduce = counted
+    try:
+        args = bench.parse_args(["--gpus", "1", "--packets", str(per_rank), "--steps", str(steps), "--warmup", "1",
+                                 "--no-cpu", "--no-e2e", "--no-replay", "--no-bpf", "--no-pmc"])
+        line = bench.run(args, 0, 1, torch.device("cuda", 0), "device")
+    finally:
+        dist.all_reduce = real
+    line["_backend"] = dist.get_backend()
+    line["_allreduce_devices"] = calls
+    with open(out, "w") as f:
+        json.dump(line, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_bench_run_rccl_one_rank(tmp_path):
+    """The N-rank path of bench.py with the backend the driver's 8-GPU run
+    uses (nccl = RCCL), at the one rank a one-GPU box allows: the line's
+    headline and legs come out of RCCL collectives on GPU tensors, and the
+    all-reduced counters equal the oracle's over the shard x the steps."""
+    import json
+    import nsd
+    per_rank, steps = 1 << 16, 3
+    out = str(tmp_path / "line.json")
+    mp.spawn(_nccl_worker, args=(1, nsd_dist.free_port(), per_rank, steps, out), nprocs=1, join=True)
+    with open(out) as f:
+        line = json.load(f)
+    assert line["_backend"] == "nccl"
+    assert line["_allreduce_devices"] and set(line["_allreduce_devices"]) == {"cuda"}
+    assert line["n_gpus"] == 1 and line["counters_total"] == per_rank * steps
+    assert set(line["legs"]) == {"imix", "ipv6x"}
+    for key, cfg in (("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):
+        leg = line["legs"][key]
+        frames, desc = T.make_batch(cfg, per_rank)
+        _, _, want, _ = T.oracle_records(frames, desc)
+        assert leg["counters"] == nsd.unpack_counters(want * np.uint64(steps)), key
