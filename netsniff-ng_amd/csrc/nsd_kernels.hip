@@ -542,11 +542,12 @@ struct HeldSt {
 // waits count the loop's loads alone; loads complete in order among
 // themselves, so a wait that leaves N later loads outstanding still covers
 // the load it waits for, whatever the stores do.  Their completion is ours:
-// drain_stores() before anything reads what they wrote.  The record stores
-// use the sc1 policy (written through, the line dropped from the XCD's L2;
-// MI355X_MICROARCH.md "stores of each flavour"): C2 0.2069 - 0.2092 ->
-// 0.2036 - 0.2049 ms against nontemporal stores on one box (records are read
-// by the host or another kernel, never by this wave again).  A store of more
+// drain_stores() before anything reads what they wrote.  The compact record
+// stores use the sc1 policy (written through, the line dropped from the
+// XCD's L2; MI355X_MICROARCH.md "stores of each flavour"): C2 0.2069 - 0.2092
+// -> 0.2036 - 0.2049 ms against nontemporal stores on one box (records are
+// read by the host or another kernel, never by this wave again); the 16-byte
+// records stay nontemporal (sc1 there: +12 %).  A store of more
 // than 8 bytes reads its data registers over two cycles, and hipcc's hazard
 // recognizer does not know an asm statement is such a store: the next VALU
 // could overwrite the data before it is read (gfx9's 12-dword store hazard;
@@ -593,7 +594,9 @@ __device__ __forceinline__ void put_rec_st(void *rec, uint32_t i, const WalkOut 
 	} else {
 		const uint4 r = pack_record(w);
 		const v4u v = { r.x, r.y, r.z, r.w };
-		asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"((uint4 *)rec + i), "v"(v) : "memory");
+		// (16-byte records stay nontemporal: with sc1 0.2667 - 0.2677 ms
+		// against 0.2370 - 0.2378)
+		asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"((uint4 *)rec + i), "v"(v) : "memory");
 	}
 }
 
