@@ -53,6 +53,9 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #ifndef NSD_CSUM_U
 #define NSD_CSUM_U 12              // interior chunk loads in flight per lane (icmp_pass)
 #endif
+#ifndef NSD_CSUM_LANES
+#define NSD_CSUM_LANES 8           // lanes per message in icmp_pass (each group instruction: 8 = one 128-B line)
+#endif
 #ifndef NSD_MINW
 #define NSD_MINW 4                 // waves per SIMD the fused kernel is register-allocated for
 #endif
@@ -1123,14 +1126,15 @@ __device__ __forceinline__ void plain4_count(uint32_t *s_ops, FlagCnt &fc, const
 // them in flight per lane; sub-lanes 0 and 1 also take the message's first
 // and last chunk with the bytes outside the message masked.  A message then
 // costs a few wave instructions per KiB instead of one wave per message.
-template <int U, bool CR>
+template <int U, bool CR, int L = NSD_CSUM_LANES>
 __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict__ frames,
 					  const uint64_t *__restrict__ desc, void *__restrict__ rec,
 					  const uint64_t *__restrict__ pend, uint32_t region)
 {
 	const int lane = threadIdx.x & 63;
 	const int wv = threadIdx.x >> 6;
-	const uint32_t sub = lane & 7, grp = lane >> 3;
+	static_assert(L == 4 || L == 8 || L == 16, "lanes per message");
+	const uint32_t sub = lane & (L - 1), grp = lane / L;
 	uint32_t bad = 0;
 	for (int l = 0; l < WAVES; l++) {
 		const uint32_t cnt = sh.pcnt[l];
@@ -1143,7 +1147,7 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 			const uint32_t moff = (uint32_t)(e >> 32) & 0xFFFF, mlen = (uint32_t)(e >> 48);
 			const uint64_t a = (on ? NSD_DESC_OFF(desc[i]) : 0) + moff;
 			const uint32_t nb = on ? (mlen & ~1u) : 0u;
-			for (uint32_t q = 0; q < 64 && k0 + q < cnt; q += 8) {
+			for (uint32_t q = 0; q < 64 && k0 + q < cnt; q += 64 / L) {
 				const int src = (int)(q + grp);
 				const uint32_t alo = __shfl((uint32_t)a, src, 64);
 				const uint32_t ahi = __shfl((uint32_t)(a >> 32), src, 64);
@@ -1158,11 +1162,11 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 				if ((sub == 0 && nch > 0) || (sub == 1 && nch > 1))
 					sum = csum_chunk(base[je], 16 * je, s0, endb);
 				// interior chunks [1, nch - 1)
-				for (uint32_t j = 1 + sub; __ballot(j + 1 < nch); j += 8 * U) {
+				for (uint32_t j = 1 + sub; __ballot(j + 1 < nch); j += L * U) {
 					uint4 v[U];
 #pragma unroll
 					for (int u = 0; u < U; u++) {
-						const uint32_t jj = j + 8 * u;
+						const uint32_t jj = j + L * u;
 						v[u] = jj + 1 < nch ? base[jj] : make_uint4(0, 0, 0, 0);
 					}
 #pragma unroll
@@ -1174,9 +1178,9 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 					}
 				}
 				sum = (sum >> 16) + (sum & 0xffff);   // folding keeps the zero test
-				sum += __shfl_xor(sum, 1, 64);
-				sum += __shfl_xor(sum, 2, 64);
-				sum += __shfl_xor(sum, 4, 64);
+#pragma unroll
+				for (int x = 1; x < L; x <<= 1)
+					sum += __shfl_xor(sum, x, 64);
 				const uint32_t mi = __shfl(i, src, 64);
 				const bool isbad = mon && sub == 0 && csum_final(sum) != 0;
 				if (isbad) {
