@@ -106,8 +106,8 @@ def test_full_size_properties(cfg):
 
 
 # ---- the compact record form (nsd_crec: the form bench.py times) -------------------
-def _run_compact(torch, f, d):
-    crec, ext, used, cnt = nsd.dissect_device_compact(f, d, mode=T.PRINT_NORM)
+def _run_compact(torch, f, d, mode=T.PRINT_NORM):
+    crec, ext, used, cnt = nsd.dissect_device_compact(f, d, mode=mode)
     torch.cuda.synchronize()
     n = d.numel()
     return (crec.cpu().numpy().view(nsd.CREC_DTYPE).copy(),
@@ -210,4 +210,32 @@ def test_full_size_compact(cfg):
         assert half == _cids(crec, pool, i)
 
     # counters = the tally over every chain
+    assert np.array_equal(cnt[:32], _compact_ops(crec, pool))
+
+
+@pytest.mark.parametrize("cfg", [T.SYN_IMIX, T.SYN_IPV6X])
+def test_full_size_compact_less(cfg):
+    """PRINT_LESS at 16,777,216 packets, compact records (the chain without
+    the IPv4 trim and checksum, Mobility without its sub-type pulls, ICMPv6
+    without its bodies: dissector.c:22-41): sampled
+    records equal nsd.compact_of(oracle in PRINT_LESS), counters = the tally
+    over every chain."""
+    import torch
+    frames, desc = T.make_batch(cfg, N, threads=16)
+    f = torch.from_numpy(frames).cuda()
+    d = torch.from_numpy(desc.view(np.int64)).cuda()
+    crec, pool, cnt = _run_compact(torch, f, d, mode=T.PRINT_LESS)
+    assert int(cnt[nsd.CNT_PKTS]) == N and int(cnt[nsd.CNT_OVERFLOW]) == 0
+    rng = np.random.default_rng(cfg + 200)
+    idx = np.unique(np.concatenate([rng.integers(0, N, 1 << 16), np.arange(4096), np.arange(N - 4096, N)]))
+    orec, oext, _, _ = T.oracle_records(frames, desc[idx], mode=T.PRINT_LESS)
+    want, _ = nsd.compact_of(orec, oext)
+    got = crec[idx]
+    for fld in ("ip_csum", "nflags", "nlayers"):
+        bad = np.nonzero(got[fld] != want[fld])[0]
+        assert len(bad) == 0, f"{fld} differs at packets {idx[bad[:10]]}"
+    inline = (want["nflags"] & 7) != 7
+    assert np.array_equal(got["chain"][inline], want["chain"][inline])
+    for k in np.nonzero(~inline)[0]:
+        assert _cids(crec, pool, int(idx[k])) == _chain(orec, oext, int(k))[0], f"chain differs at {idx[k]}"
     assert np.array_equal(cnt[:32], _compact_ops(crec, pool))
