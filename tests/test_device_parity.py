@@ -622,3 +622,40 @@ def test_graph_capture_and_replay(compact, schedule_small):
             orec, oext, ocnt, _ = T.oracle_records(f, d, mode=T.PRINT_NORM)
             assert_same_records(drec, orec, dext, oext)
             assert np.array_equal(cnt.cpu().numpy().view(np.uint64), ocnt)
+
+
+def _cut_sweep(align=16):
+    """Every packet of the edge set, 64 C4 and 32 IMIX samples, each cut at
+    every capture length up to 160 bytes (and a few past): the batch holds
+    the WHOLE original packet at each offset with the descriptor's caplen
+    set to the cut, so the bytes right past caplen are exactly the headers a
+    walk that ignored caplen would go on to parse.  The device's
+    continuation windows are not zeroed past caplen and its 4-byte layer
+    reads do not mask them (nsd_kernels.hip LSrc::dword_at: every use is
+    gated by the layer's pull); this is the test of that argument."""
+    base = [p for p in edge_cases.cases() if 0 < len(p) <= 600]
+    for cfg, n in ((T.SYN_IPV6X, 64), (T.SYN_IMIX, 32)):
+        fr, de = T.make_batch(cfg, n)
+        base += [bytes(fr[int(d) & 0xFFFFFFFFFF:(int(d) & 0xFFFFFFFFFF) + (int(d) >> 40)]) for d in de]
+    offs, lens, off = [], [], 0
+    for p in base:
+        cuts = list(range(0, min(len(p), 160) + 1)) + [c for c in (200, 300, 400) if c < len(p)]
+        for c in cuts:
+            off = (off + align - 1) & ~(align - 1)
+            offs.append((off, p))
+            lens.append(c)
+            off += len(p)
+    frames = np.zeros(off + 64, dtype=np.uint8)
+    desc = np.zeros(len(offs), dtype=np.uint64)
+    for i, ((o, p), c) in enumerate(zip(offs, lens)):
+        frames[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+        desc[i] = T.desc_pack(o, c)
+    return frames, desc
+
+
+@pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
+def test_cut_sweep_live_tails(mode):
+    frames, desc = _cut_sweep()
+    assert len(desc) > 20000
+    _check(frames, desc, mode)
+    _check_compact(frames, desc, mode)
