@@ -49,6 +49,42 @@ def main():
             r = b.roofline(ms)
             print(f"{key:6s} rec{b.rec_b:<2d} {nsd.last_schedule()} kernel_ms={ms:.4f} frac={r['frac'] if r else None} "
                   f"read_frac={r['read_frac'] if r else None} pkts_counted={int(cnt[32])}", flush=True)
+            if os.environ.get("KB_ENDS"):
+                # counters 56..61 of an instrumented variant (a timeline patch):
+                # ~min / max of block start, wave tile-phase end, block end
+                # (s_memrealtime, 100 MHz), one more launch with zeroed counters
+                b.counters.zero_()
+                b.step(args.mode, 0 if compact else args.grid, zero=False)
+                b.sync()
+                c = b.counters.cpu().numpy().view(np.uint64)
+                inv = lambda x: int(~np.uint64(x))   # noqa: E731
+                t0 = inv(c[56])
+                us = lambda t: round((t - t0) / 100.0, 1)   # noqa: E731
+                print(f"{key:6s} timeline_us start {us(t0)}..{us(int(c[57]))} tiles_end {us(inv(c[58]))}.."
+                      f"{us(int(c[59]))} block_end {us(inv(c[60]))}..{us(int(c[61]))}", flush=True)
+                if os.environ.get("KB_ENDS") == "xcd":
+                    print(f"{key:6s} per-XCD (block % 8) last tile-phase end {[us(int(x)) for x in c[40:48]]} "
+                          f"last block end {[us(int(x)) for x in c[48:56]]}", flush=True)
+            if os.environ.get("KB_DBG"):
+                # a variant with per-wave start / tile-phase end times (g_dbg,
+                # nsd_dbg_read): one more launch, then the spread within and
+                # across blocks
+                import ctypes
+                b.step(args.mode, 0 if compact else args.grid, zero=False)
+                b.sync()
+                buf = np.zeros(3 * 16384, dtype=np.uint64)
+                assert nsd.lib().nsd_dbg_read(ctypes.c_void_p(buf.ctypes.data)) == 0
+                st, en = buf[:16384].astype(np.int64), buf[16384:32768].astype(np.int64)
+                nw = int(np.count_nonzero(st))
+                st, en = st[:nw], en[:nw]
+                t = (en - st.min()) / 100.0
+                blk = t.reshape(-1, 4)
+                print(f"{key:6s} waves {nw}: tile-phase end us p0 {t.min():.1f} p10 {np.percentile(t, 10):.1f} "
+                      f"p50 {np.median(t):.1f} p90 {np.percentile(t, 90):.1f} p100 {t.max():.1f}; within-block "
+                      f"spread mean {np.mean(blk.max(1) - blk.min(1)):.1f}, block means' spread "
+                      f"{blk.mean(1).max() - blk.mean(1).min():.1f}; wave-in-block means "
+                      f"{[round(float(x), 1) for x in blk.mean(0)]}", flush=True)
+                np.save(os.path.join(ROOT, "gpurun_out", "var", f"dbg_{key}.npy"), buf[:32768])
             if os.environ.get("KB_PHASES"):
                 # counters 48..55 of an instrumented variant (tools/variants/phases.patch),
                 # summed over waves, last launch: fast-walk part, walker engine, window
