@@ -53,6 +53,9 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #ifndef NSD_CSUM_U
 #define NSD_CSUM_U 12              // interior chunk loads in flight per lane (icmp_pass)
 #endif
+#ifndef NSD_GROUP_TILES
+#define NSD_GROUP_TILES 1          // fused waves take their tiles at run time from a counter per CU group
+#endif
 #ifndef NSD_PRIO
 #define NSD_PRIO 1                 // fused waves' issue priority by their tile progress (walk_tiles)
 #endif
@@ -1229,7 +1232,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 					   void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 					   uint32_t *__restrict__ ext_used, uint32_t chunk,
 					   const uint32_t *__restrict__ sll, Pending &pq,
-					   unsigned long long *__restrict__ sched)
+					   unsigned long long *__restrict__ sched, uint32_t *__restrict__ gtiles)
 {
 	constexpr int ROW = row_of(WIN1);
 	auto &s_win = sh.win;
@@ -1267,12 +1270,74 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 		return;
 	}
 
+	// Tiles of a CU group.  A launch of 4 blocks per CU places blocks b,
+	// b + G, b + 2G, b + 3G (G = grid / 4) on one CU, and the SIMD arbiter
+	// runs the first-placed block's waves ahead of the later ones (C4: the
+	// rounds ended their tiles at 835 / 881 / 945 / 1031 us).  So the group's
+	// 16 waves share its grid-stride tiles: the group's j-th tile is row
+	// j / 16 of the grid stride, block b + ((j / 4) % 4) G, wave j % 4 (the
+	// static order, so the waves still sweep the batch front to back, and
+	// tile numbers grow with j), and a wave takes the next j from the
+	// group's counter (a line of its own in the workspace, zeroed before
+	// each launch by zero_tiles; one counter for the whole grid serialised
+	// its atomics: 2.3x slower).
+	// The atomic for tile t+2 is issued a tile ahead and its return read then
+	// (hipcc's atomic optimizer would wait for it at once: the offset it
+	// cannot prove uniform).  A wave asks only while its pending list has
+	// room for an entry from every packet of the tiles it holds, the new one
+	// and its walkers: the lists hold twice a wave's even share plus four
+	// tiles (region_for_fused), so a group's waves cannot all stop for room
+	// while its tiles are left.  Grids that are not 4 blocks per CU share
+	// per block.  Compact records only (the 16-byte form's walk state leaves
+	// no registers for it: 12 VGPRs spilled).
+	constexpr bool DYN = NSD_GROUP_TILES && CR;
+	const uint32_t ntiles = (n + 63) / 64;
+	const uint32_t nw = gridDim.x * WAVES;
+	const bool grp4 = (gridDim.x & 3) == 0;
+	const uint32_t G = grp4 ? gridDim.x / 4 : gridDim.x, R = grp4 ? 4u : 1u;
+	const uint32_t grp = blockIdx.x % G;
+	uint32_t *const gctr = gtiles + 32 * grp;
+	auto tile_of = [&](uint32_t j) -> uint32_t {   // the group's j-th tile's first packet (n: none)
+		const uint32_t k = j / (4 * R), r = (j / 4) % R, w = j % 4;
+		const uint64_t t = (uint64_t)k * nw + (grp + r * G) * 4 + w;
+		return t < ntiles ? (uint32_t)t * 64 : n;
+	};
+	uint32_t gv = 0;
+	bool asked = false;
+	auto ask = [&](uint32_t held) {
+		const uint32_t used = pq.npend + pq.nleaf;
+		asked = used + 64u * (held + 2) <= pq.wcap;
+		if (asked && lane == 0) {
+			uint32_t z;
+			asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+			gv = atomicAdd(gctr + z, 1u);
+		}
+	};
+	auto take = [&]() -> uint32_t {   // the asked tile (n: none)
+		if (!asked)
+			return n;
+		asked = false;
+		return tile_of((uint32_t)__builtin_amdgcn_readfirstlane((int)gv));
+	};
+	uint32_t nb1 = n, nb2 = n;
+	if constexpr (DYN) {
+		ask(0);
+		base = take();
+		if (base < n) {
+			ask(1);
+			nb1 = take();
+			if (nb1 < n)
+				ask(2);   // for tile t+2, read when tile t is walked
+		}
+	} else {
+		nb1 = base + stride < n ? base + stride : n;
+	}
 	// software pipeline: tile t walked while tile t+1's chunks and tile t+2's
 	// descriptors are in flight
 	if (base >= n)
 		return;
 	uint64_t d0 = (base + lane < n) ? desc[base + lane] : 0;
-	uint64_t d1 = (base + stride < n && base + stride + lane < n) ? desc[base + stride + lane] : 0;
+	uint64_t d1 = (nb1 < n && nb1 + lane < n) ? desc[nb1 + lane] : 0;
 	Chunks<WIN1> ch;
 	stage_load<WIN1>(ch, frames, d0, lane);
 	Walker wk;
@@ -1291,11 +1356,11 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	hs.ri = hs.pp = 0xFFFFFFFFu;
 	// (one more pass after the last tile drains the walkers: the engine is
 	// inlined once)
-	// this wave's tiles (grid-stride) and the ones walked, for prio_level
-	const uint32_t share = base < n ? (n - base + stride - 1) / stride : 1u;
+	// this wave's even share of tiles and the ones walked, for prio_level
+	const uint32_t share = (ntiles + nw - 1) / nw;
 	uint32_t done = 0, lvl = 0xFFu;
-	for (;; base += stride) {
-		if (NSD_PRIO) {
+	for (;;) {
+		if (NSD_PRIO && CR) {   // (the 16-byte form's walk state leaves no registers for it)
 			const uint32_t l = done < share ? 4u * done / share : 3u;
 			if (l != lvl) {
 				lvl = l;
@@ -1316,9 +1381,14 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			stage_write(&s_win[wv][0], ch, lane);
 			hs.flush(rec, wq);   // tile t-1's stores, before tile t+1's loads
 			// prefetch: descriptors of tile t+2, chunks of tile t+1
-			const uint32_t b2 = base + 2 * stride;
+			if constexpr (DYN) {
+				nb2 = take();
+				if (nb2 < n)
+					ask(3);   // tiles t .. t+2 held
+			}
+			const uint32_t b2 = DYN ? nb2 : base + 2 * stride;
 			d2 = (b2 < n && b2 + lane < n) ? desc[b2 + lane] : 0;
-			const uint32_t b1 = base + stride;
+			const uint32_t b1 = DYN ? nb1 : base + stride;
 			if (b1 < n && !late)
 				stage_load<WIN1>(ch, frames, d1, lane);
 			wave_sync_lds();
@@ -1427,7 +1497,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 		// ahead, those lines had left L2 by the time the walkers staged them:
 		// C4 400 -> 349 B/packet, 1.152 -> 1.107 ms on one box).  The chunk
 		// registers are dead during the walkers either way.
-		if (late && base + stride < n)
+		if (late && (DYN ? nb1 : base + stride) < n)
 			stage_load<WIN1, false, false>(ch, frames, d1, lane);
 		// (NSD_LATE 0: the chunks load a tile ahead, and while the walkers are
 		// busy the lines of tile t+2 go into L2 now, so the next iteration's
@@ -1436,13 +1506,20 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 		// would wait for the touches (vector memory counts in order; C2
 		// +12 %).  The LDS-DMA target is window words past the fast rows.)
 		{
-			const uint32_t b2 = base + 2 * stride;
+			const uint32_t b2 = DYN ? nb2 : base + 2 * stride;
 			if (!NSD_LATE && many && b2 < n)
 				l2_touch(frames, d2, &s_win[wv][64 * ROW], b2 + lane < n);
 		}
 		late = NSD_LATE && many;
 		d0 = d1;
 		d1 = d2;
+		if constexpr (DYN) {
+			base = nb1;
+			nb1 = nb2;
+			nb2 = n;
+		} else {
+			base += stride;
+		}
 	}
 	fc.flush(s_cnt, lane);
 	// the schedule sample (a launch the launcher samples passes its pair)
@@ -1504,13 +1581,24 @@ __device__ __forceinline__ void leaf_pass(const uint8_t *__restrict__ frames, co
 // left pending, then sums the ICMPv4 messages they left pending; a later
 // phase reads only what the same block wrote (its pending lists), so the
 // phases need a block barrier, not a grid-wide one.
+// the fused launch's group tile counters (walk_tiles): word 0 of each
+// 128-byte line.  A kernel rather than hipMemsetAsync: with the memset
+// captured into a HIP graph the counters held garbage from the second
+// replay on (tools/dbg_graph.py), so no tile was walked.
+__global__ void zero_tiles(uint32_t *__restrict__ gtiles, uint32_t groups)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < groups)
+		gtiles[32 * i] = 0;
+}
+
 template <int MODE, bool CR>
 __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 	void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
 	uint64_t *__restrict__ pend, uint32_t region, const uint32_t *__restrict__ sll,
-	unsigned long long *__restrict__ sched)
+	unsigned long long *__restrict__ sched, uint32_t *__restrict__ gtiles)
 {
 	__shared__ Shared sh;
 	if (threadIdx.x < 64)
@@ -1524,7 +1612,8 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	// this wave's pending list (a wave visits region / WAVES packets)
 	Pending pq{ pend + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (region / WAVES), region / WAVES, 0,
 		    0 };
-	walk_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq, sched);
+	walk_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq, sched,
+			     gtiles);
 	if (MODE == PRINT_NORM || MODE == PRINT_LESS)
 		leaf_pass<MODE, CR>(frames, desc, rec, ext, pq);
 	if ((threadIdx.x & 63) == 0)
@@ -2216,6 +2305,14 @@ static uint32_t region_for(uint32_t n, uint32_t blocks)
 	const uint64_t stride = (uint64_t)blocks * nsd::BLOCK;
 	return (uint32_t)(((n + stride - 1) / stride) * nsd::BLOCK);
 }
+// the fused kernel's pending-list slots per block: its waves take their
+// group's tiles at run time (walk_tiles, compact records), so each list holds twice a wave's
+// even share plus four tiles (8 bytes a slot: within the workspace's first
+// 32 bytes per region slot, sched_pair_at)
+static uint32_t region_for_fused(uint32_t n, uint32_t blocks, bool compact)
+{
+	return NSD_GROUP_TILES && compact ? 2 * region_for(n, blocks) + nsd::WAVES * 4 * 64 : region_for(n, blocks);
+}
 
 // worst case over grids: sum of regions <= n + blocks * BLOCK
 static size_t region_slots(uint32_t n)
@@ -2398,10 +2495,16 @@ extern "C" int nsd_last_schedule(void)
 // walker kernel's pending lists (u64 per slot, up to two per packet slot)
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // (the last 256 bytes: the schedule sample's pair, at sched_pair_at)
-static size_t sched_pair_at(uint32_t n)
+// (then the fused kernel's group tile counters: a 128-byte line per block
+// at most, gtiles_at)
+static size_t gtiles_at(uint32_t n)
 {
 	const size_t slots = region_slots(n);
 	return align256(align256(32 * slots) + align256((size_t)NSD_MAX_GRID * nsd::WAVES * 8) + 16 * slots);
+}
+static size_t sched_pair_at(uint32_t n)
+{
+	return gtiles_at(n) + (size_t)NSD_MAX_GRID * 128;
 }
 extern "C" size_t nsd_launch_workspace_bytes(uint32_t n)
 {
@@ -2481,7 +2584,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	if (fused) {
 	typedef void (*kfn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, uint32_t *, uint32_t,
 			    uint32_t *, uint32_t, unsigned long long *, uint64_t *, uint32_t, const uint32_t *,
-			    unsigned long long *);
+			    unsigned long long *, uint32_t *);
 	static const kfn kernels[2][3] = {
 		{ dissect_all<PRINT_NORM, false>, dissect_all<PRINT_LESS, false>, dissect_all<PRINT_HEX, false> },
 		{ dissect_all<PRINT_NORM, true>, dissect_all<PRINT_LESS, true>, dissect_all<PRINT_HEX, true> },
@@ -2492,9 +2595,20 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	if (cap_blocks > NSD_MAX_GRID)
 		cap_blocks = NSD_MAX_GRID;
 	const uint32_t blocks = want < cap_blocks ? want : cap_blocks;
+	// the CU groups' tile counters (walk_tiles), a 128-byte line each, zeroed
+	// on the launch's stream
+	uint32_t *const gtiles = (uint32_t *)((uint8_t *)d_ws + gtiles_at(n));
+	if (NSD_GROUP_TILES && compact) {
+		hipLaunchKernelGGL(zero_tiles, dim3((blocks + 255) / 256), dim3(256), 0, stream, gtiles, blocks);
+		if (hipGetLastError() != hipSuccess) {
+			if (sched)
+				sched_abort();
+			return -2;
+		}
+	}
 	hipLaunchKernelGGL(f, dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec, d_ext,
 			   ext_words, d_ext_used, chunk_for(blocks), (unsigned long long *)d_counters, (uint64_t *)d_ws,
-			   region_for(n, blocks), (const uint32_t *)d_sll, sched);
+			   region_for_fused(n, blocks, compact), (const uint32_t *)d_sll, sched, gtiles);
 	if (hipGetLastError() != hipSuccess) {
 		if (sched)
 			sched_abort();
