@@ -63,7 +63,7 @@ def main():
                 print(f"{key:6s} timeline_us start {us(t0)}..{us(int(c[57]))} tiles_end {us(inv(c[58]))}.."
                       f"{us(int(c[59]))} block_end {us(inv(c[60]))}..{us(int(c[61]))}", flush=True)
                 if os.environ.get("KB_ENDS") == "xcd":
-                    print(f"{key:6s} per-XCD (block % 8) last tile-phase end {[us(int(x)) for x in c[40:48]]} "
+                    print(f"{key:6s} per-group (block * 4 / grid: dispatch round) last tile-phase end {[us(int(x)) for x in c[40:48]]} "
                           f"last block end {[us(int(x)) for x in c[48:56]]}", flush=True)
             if os.environ.get("KB_DBG"):
                 # a variant with per-wave start / tile-phase end times (g_dbg,
@@ -84,7 +84,7 @@ def main():
                       f"spread mean {np.mean(blk.max(1) - blk.min(1)):.1f}, block means' spread "
                       f"{blk.mean(1).max() - blk.mean(1).min():.1f}; wave-in-block means "
                       f"{[round(float(x), 1) for x in blk.mean(0)]}", flush=True)
-                np.save(os.path.join(ROOT, "gpurun_out", "var", f"dbg_{key}.npy"), buf[:32768])
+                np.save(os.path.join(ROOT, "gpurun_out", "var", f"dbg_{key}.npy"), buf)
             if os.environ.get("KB_PHASES"):
                 # counters 48..55 of an instrumented variant (tools/variants/phases.patch),
                 # summed over waves, last launch: fast-walk part, walker engine, window
