@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--records", default="both", choices=["compact", "full", "both"])
     ap.add_argument("--sched", default="adaptive", choices=["adaptive", "split", "fused"],
                     help="kernel schedule (nsd_set_schedule)")
+    ap.add_argument("--bpf", action="store_true", help="also time the device BPF filter (bench.bpf_bench: "
+                    "verdicts, and with the compaction, whose accepted count it checks)")
     ap.add_argument("--lib", default=None, help="a variant libnsdissect.so (tools/build_variant.sh) "
                     "loaded instead of the in-tree one (dev tools only; the product loads its own)")
     args = ap.parse_args()
@@ -44,6 +46,10 @@ def main():
     for key in args.configs.split(","):
         for compact in forms:
             b = bench.Batch(key, args.packets, 0, 1, dev, compact=compact)
+            if args.bpf:
+                r = bench.bpf_bench(b, args.steps, args.warmup)
+                print(f"{key:6s} bpf kernel_ms={r['kernel_ms']:.4f} compact_ms={r['compact_ms']:.4f} "
+                      f"frac={r['roofline']['frac']} accepted={r['accepted']}", flush=True)
             ms = bench.time_steps(b, args.mode, args.steps, args.warmup, 0 if compact else args.grid)
             cnt = b.counters.cpu().numpy().view(np.uint64)
             r = b.roofline(ms)
