@@ -354,10 +354,12 @@ def test_device_random_programs():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg,n", [(T.SYN_IMIX, 100000), (T.SYN_UDP64, 3000), (T.SYN_IPV6X, 1),
-                                   (T.SYN_IMIX, 1024), (T.SYN_IMIX, 1025), (T.SYN_IMIX, 3 << 20)])
+                                   (T.SYN_IMIX, 1024), (T.SYN_IMIX, 1025), (T.SYN_IMIX, 3 << 20),
+                                   (T.SYN_IMIX, (4 << 20) + 4097)])
 def test_device_compaction(cfg, n):
     """Device-resident filter with compaction: verdicts identical to the
-    oracle's, the accepted descriptors packed in batch order."""
+    oracle's, the accepted descriptors packed in batch order (the last size:
+    16,401 per-block counts, so the count scan takes a second, ragged pass)."""
     import torch
     frames, desc = T.make_batch(cfg, n)
     p = P_TCP if cfg != T.SYN_IPV6X else P_ALL
