@@ -27,8 +27,8 @@ def native_build():
 def _schedule(request):
     import nsd
     prev = nsd.set_schedule(nsd.SCHED_SPLIT if request.param == "split" else nsd.SCHED_FUSED)
-    if request.param == "fused_grid3":
-        nsd.set_grid_cap(3)
+    if request.param.startswith("fused_grid"):
+        nsd.set_grid_cap(int(request.param[len("fused_grid"):]))
     yield request.param
     nsd.set_schedule(prev)
     nsd.set_grid_cap(0)
@@ -42,10 +42,12 @@ def schedule(request):
     yield from _schedule(request)
 
 
-@pytest.fixture(params=["split", "fused", "fused_grid3"])
+@pytest.fixture(params=["split", "fused", "fused_grid3", "fused_grid8"])
 def schedule_small(request):
     """`schedule` for small batches, plus the fused kernel with its grid
     capped at 3 blocks (nsd_set_grid_cap), so each wave walks many tiles:
     walkers carried across tiles, the pending lists of many tiles, waves of
-    a block with unequal tile counts."""
+    a block with unequal tile counts; and at 8 blocks: two CU groups of four
+    blocks sharing their tiles through the group counters (walk_tiles), with
+    many tiles per wave."""
     yield from _schedule(request)
