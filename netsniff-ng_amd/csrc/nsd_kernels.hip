@@ -1213,7 +1213,10 @@ __device__ __forceinline__ void icmp_pass(Shared &sh, const uint8_t *__restrict_
 // one block per CU: with 4 blocks per CU the first round finished its tiles
 // 20 % ahead of the fourth (C4: 835 against 1031 us; C3: 305 against 422),
 // whose waves then ran the launch's tail with the CU a quarter full.
-// (Priority by round alone only swapped which round lagged.)
+// (Priority by round alone only swapped which round lagged.)  Since the
+// group tiles balance a CU's blocks, it still gives C3 0.7 % but costs
+// walker-heavy batches 1 % (C4): the launcher turns it off for those
+// (`prio`, from the schedule sample).
 __device__ __forceinline__ void prio_level(uint32_t lvl)
 {
 	if (lvl == 0)
@@ -1232,7 +1235,8 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 					   void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 					   uint32_t *__restrict__ ext_used, uint32_t chunk,
 					   const uint32_t *__restrict__ sll, Pending &pq,
-					   unsigned long long *__restrict__ sched, uint32_t *__restrict__ gtiles)
+					   unsigned long long *__restrict__ sched, uint32_t *__restrict__ gtiles,
+					   uint32_t prio)
 {
 	constexpr int ROW = row_of(WIN1);
 	auto &s_win = sh.win;
@@ -1360,7 +1364,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	const uint32_t share = (ntiles + nw - 1) / nw;
 	uint32_t done = 0, lvl = 0xFFu;
 	for (;;) {
-		if (NSD_PRIO && CR) {   // (the 16-byte form's walk state leaves no registers for it)
+		if (NSD_PRIO && CR && prio) {   // (the 16-byte form's walk state leaves no registers for it)
 			const uint32_t l = done < share ? 4u * done / share : 3u;
 			if (l != lvl) {
 				lvl = l;
@@ -1598,7 +1602,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
 	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
 	uint64_t *__restrict__ pend, uint32_t region, const uint32_t *__restrict__ sll,
-	unsigned long long *__restrict__ sched, uint32_t *__restrict__ gtiles)
+	unsigned long long *__restrict__ sched, uint32_t *__restrict__ gtiles, uint32_t prio)
 {
 	__shared__ Shared sh;
 	if (threadIdx.x < 64)
@@ -1613,7 +1617,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	Pending pq{ pend + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (region / WAVES), region / WAVES, 0,
 		    0 };
 	walk_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq, sched,
-			     gtiles);
+			     gtiles, prio);
 	if (MODE == PRINT_NORM || MODE == PRINT_LESS)
 		leaf_pass<MODE, CR>(frames, desc, rec, ext, pq);
 	if ((threadIdx.x & 63) == 0)
@@ -2348,8 +2352,10 @@ static size_t region_slots(uint32_t n)
 // average at most NSD_SMALL_FRAME bytes, the fast kernel runs
 // NSD_FAST_BPC_SMALL blocks per CU instead of NSD_FAST_BPC (C2's 64-byte
 // frames stream from few waves: 0.217 -> 0.207 ms at 2 blocks per CU on one
-// box, where IMIX frames need the third: 0.78 against 0.92 ms).  State is
-// per device.
+// box, where IMIX frames need the third: 0.78 against 0.92 ms); and when
+// more than a quarter of its packets went to the walkers, the fused kernel
+// runs without the progress priority (walk_tiles: C4 -1 % without it, C3
+// +0.7 %, in the same kernel).  State is per device.
 #ifndef NSD_SCHED_SAMPLE
 #define NSD_SCHED_SAMPLE 32
 #endif
@@ -2363,6 +2369,7 @@ constexpr int MAX_DEV = 16;
 #endif
 struct Sched {
 	bool init = false, fused = false, pending = false, small = false;
+	bool walky = false;                    // the sample's deferred share above 25 % (no progress priority)
 	bool recorded = false;                 // the pending sample's event is recorded (sched_sampled)
 	int launches = 0, last = 0;
 	uint64_t sampled = 0;                  // packets of the sampled launch in flight
@@ -2387,7 +2394,7 @@ int cur_dev()
 // and whether this launch is the sample (then its pair is zeroed on
 // `stream` here and copied back by sched_sampled after the kernels).
 struct Plan {
-	bool fused, sample, small;
+	bool fused, sample, small, prio;
 	int cus;
 };
 Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, hipStream_t stream)
@@ -2401,7 +2408,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 			cus = 256;
 		S.cus = cus;
 	}
-	Plan p{ false, false, false, S.cus };
+	Plan p{ false, false, false, true, S.cus };
 	// a launch captured into a graph takes the schedule as it stands and is
 	// never the sample (an event query or a host copy would break the
 	// capture; the graph replays this plan)
@@ -2417,6 +2424,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 		const uint64_t pk = S.host[4] - S.host[2], by = S.host[5] - S.host[3];
 		if (pk)
 			S.small = by <= (uint64_t)NSD_SMALL_FRAME * pk;
+		S.walky = rd > 0.25;
 		S.pending = false;
 		S.recorded = false;
 	}
@@ -2428,6 +2436,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 	}
 	p.fused = g_sched_force ? g_sched_force == NSD_SCHED_FUSED : S.fused;
 	p.small = S.small;
+	p.prio = !S.walky;
 	if (!capturing && ++S.launches >= NSD_SCHED_SAMPLE && !S.pending && S.host && pair && counters &&
 	    hipMemsetAsync(pair, 0, 16, stream) == hipSuccess &&
 	    hipMemcpyAsync(S.host + 2, counters + NSD_CNT_PKTS, 16, hipMemcpyDeviceToHost, stream) == hipSuccess) {
@@ -2584,7 +2593,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	if (fused) {
 	typedef void (*kfn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, uint32_t *, uint32_t,
 			    uint32_t *, uint32_t, unsigned long long *, uint64_t *, uint32_t, const uint32_t *,
-			    unsigned long long *, uint32_t *);
+			    unsigned long long *, uint32_t *, uint32_t);
 	static const kfn kernels[2][3] = {
 		{ dissect_all<PRINT_NORM, false>, dissect_all<PRINT_LESS, false>, dissect_all<PRINT_HEX, false> },
 		{ dissect_all<PRINT_NORM, true>, dissect_all<PRINT_LESS, true>, dissect_all<PRINT_HEX, true> },
@@ -2608,7 +2617,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	}
 	hipLaunchKernelGGL(f, dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec, d_ext,
 			   ext_words, d_ext_used, chunk_for(blocks), (unsigned long long *)d_counters, (uint64_t *)d_ws,
-			   region_for_fused(n, blocks, compact), (const uint32_t *)d_sll, sched, gtiles);
+			   region_for_fused(n, blocks, compact), (const uint32_t *)d_sll, sched, gtiles, plan.prio ? 1u : 0u);
 	if (hipGetLastError() != hipSuccess) {
 		if (sched)
 			sched_abort();

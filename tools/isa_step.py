@@ -17,7 +17,7 @@ import subprocess
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "_ZN3nsd11dissect_allILi0ELb1EEEvPKhPKmjiPvPjjS6_jPyPmjPKjS7_"
+KERNEL = "_ZN3nsd11dissect_allILi0ELb1EEEv"   # (prefix of the mangled name)
 
 
 def classify(op):
@@ -85,7 +85,7 @@ def main():
                         "-Wno-unused-function", "--cuda-device-only", "-S", "-o", s, args.src],
                        check=True, stderr=subprocess.DEVNULL)
         text = open(s).read().split("\n")
-    i0 = next(i for i, ln in enumerate(text) if ln.startswith(KERNEL + ":"))
+    i0 = next(i for i, ln in enumerate(text) if ln.startswith(KERNEL) and ln.split(";")[0].rstrip().endswith(":"))
     i1 = next(i for i in range(i0, len(text)) if "s_endpgm" in text[i])
     fn = text[i0:i1 + 1]
     h, e = find_loop(fn)
