@@ -56,6 +56,9 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #ifndef NSD_GROUP_TILES
 #define NSD_GROUP_TILES 1          // fused waves take their tiles at run time from a counter per CU group
 #endif
+#ifndef NSD_GROUP_BLOCKS
+#define NSD_GROUP_BLOCKS 4u        // blocks sharing a tile counter (4: one CU's; 8: two CUs of one XCD)
+#endif
 #ifndef NSD_PRIO
 #define NSD_PRIO 1                 // fused waves' issue priority by their tile progress (walk_tiles)
 #endif
@@ -1297,8 +1300,8 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	constexpr bool DYN = NSD_GROUP_TILES && CR;
 	const uint32_t ntiles = (n + 63) / 64;
 	const uint32_t nw = gridDim.x * WAVES;
-	const bool grp4 = (gridDim.x & 3) == 0;
-	const uint32_t G = grp4 ? gridDim.x / 4 : gridDim.x, R = grp4 ? 4u : 1u;
+	const bool grp4 = gridDim.x % NSD_GROUP_BLOCKS == 0;
+	const uint32_t G = grp4 ? gridDim.x / NSD_GROUP_BLOCKS : gridDim.x, R = grp4 ? NSD_GROUP_BLOCKS : 1u;
 	const uint32_t grp = blockIdx.x % G;
 	uint32_t *const gctr = gtiles + 32 * grp;
 	auto tile_of = [&](uint32_t j) -> uint32_t {   // the group's j-th tile's first packet (n: none)
