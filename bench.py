@@ -100,11 +100,35 @@ def wsum_for(key, n, lo, shards=1):
     return total
 
 
+def lines_for(key, n, lo, shards=1):
+    """The line floor of [lo, lo + shards*n): distinct 128-byte lines holding
+    the bytes the chains must inspect (tests/golden/lines.json, made by
+    make_golden.py --lines-only from the CPU restatement), else None."""
+    path = os.path.join(ROOT, "tests", "golden", "lines.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        table = json.load(f)
+    total = 0
+    for r in range(shards):
+        k = f"{key}:{lo + r * n}:{n}"
+        if k not in table:
+            return None
+        total += int(table[k])
+    return total
+
+
 def library_info():
+    """The benched library: its file hash, the source hash compiled into it
+    (the Makefile's SRCHASH over csrc/*, the Makefile and the ABI header) and
+    the same hash over this tree's sources, so the line names the code that
+    produced the binary it timed."""
     L = nsd.lib()
     with open(nsd.LIB_PATH, "rb") as f:
         sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    built, tree = nsd.built_source_hash(), nsd.source_hash()
     return {"path": os.path.relpath(nsd.LIB_PATH, ROOT), "sha256_16": sha,
+            "source_sha256_16": built, "tree_source_sha256_16": tree, "source_matches_tree": built == tree,
             "version": L.nsd_version().decode(), "build": L.nsd_build_info().decode()}
 
 
@@ -118,7 +142,9 @@ class Batch:
         self.rec_b = CREC_B if compact else REC_B
         self.n = n * shards
         cfg = CONFIGS[key]["cfg"]
-        self.frames, self.desc, desc_np = T.make_device_batch(cfg, self.n, lo=lo, device=dev)
+        # (4M-packet host chunks: at 8 ranks a 16M C4 chunk each would hold
+        # 8 x 13 GB of host memory at once)
+        self.frames, self.desc, desc_np = T.make_device_batch(cfg, self.n, lo=lo, device=dev, chunk=1 << 22)
         caps = T.desc_caplen(desc_np)
         self.frame_bytes = int(caps.sum())
         self.line_bytes = int(np.minimum(caps, 64).sum())   # first 64-B line per frame (BPF leg)
@@ -132,6 +158,7 @@ class Batch:
         self.counters = torch.zeros(nsd.NCOUNTERS, dtype=torch.int64, device=dev)
         self.ws = torch.empty(nsd.lib().nsd_workspace_bytes(self.n), dtype=torch.uint8, device=dev)
         self.wsum = wsum_for(key, n, lo, shards)
+        self.lines = lines_for(key, n, lo, shards)
 
     def step(self, mode, grid=0, ev=None, zero=True):
         if zero:
@@ -164,6 +191,15 @@ class Batch:
         if traffic is not None:
             r["traffic_bytes_per_pkt"] = {"read": round(traffic["read_bytes"] / self.n, 1),
                                           "write": round(traffic["write_bytes"] / self.n, 1)}
+        if self.lines is not None:
+            # the least any schedule reading whole 128-byte lines can fetch:
+            # each needed line once, plus the descriptors
+            floor = 128 * self.lines + DESC_B * self.n
+            r["line_floor_bytes_per_pkt"] = {"read": round(floor / self.n, 2),
+                                             "source": "tests/golden/lines.json (nsor_line_floor_mt)"}
+            if traffic is not None:
+                r["traffic_vs_line_floor"] = {"read": round(traffic["read_bytes"] / floor, 3),
+                                              "write": round(traffic["write_bytes"] / (self.rec_b * self.n), 3)}
         if copy_gbs:
             r["copy_gbs"] = round(copy_gbs, 1)
             r["frac_of_copy"] = round(achieved / copy_gbs, 4)
@@ -511,13 +547,17 @@ def ref_harness_all_cores(cfg, key, procs, rate1, seconds=8.0):
 
 
 def cpu_baseline(key, seconds):
-    """The CPU restatement on this host (SURVEY 8d / BASELINE.md "CPU-baseline
-    plan"): fields + PRINT_NORM text and fields only, each on 1 thread, on
-    the GPU's 16-thread CPU share and on every available core.  `value` is
-    the text rate on all available cores (what the reference does - it
-    prints as it parses - on the whole host), `cores` that thread count.
-    Beside it, the reference's own objects (oracle/_ref/nsref) on one core
-    and as one process per core of the same share, for C2 and C3 IMIX."""
+    """The CPU baseline on this host (SURVEY 8d / BASELINE.md "CPU-baseline
+    plan").  `value` is the reference itself: its own objects
+    (oracle/_ref/nsref: pcap reader, record conversion, frame header line,
+    parser objects, tprintf.c) as one process per core of the GPU's 16-CPU
+    share over contiguous shards of the headline workload, the way the
+    reference scales out (kind "reference", `cores` the processes).  Beside
+    it: the same for C3 IMIX, the reference on one core, and the CPU
+    restatement (oracle/nsd_oracle.c, kind "port"): fields + PRINT_NORM text
+    and fields only, on 1 thread, the 16-thread share and every available
+    core.  When the reference's objects are not built, `value` falls back to
+    the port's text rate on every available core."""
     cfg = CONFIGS[key]["cfg"]
     model, nproc, avail = cpu_info()
     t16 = min(avail, 16)   # the GPU box's CPU share per GPU is 16 threads
@@ -533,17 +573,24 @@ def cpu_baseline(key, seconds):
     else:
         tA, pA, dA, fA = tS, pS, dS, fS
     ref1, refA = {}, {}
-    for k in ("udp64", "imix"):
+    for k in dict.fromkeys(("udp64", "imix", key)):
         r1 = ref_harness_rate(CONFIGS[k]["cfg"], k, n=(1 << 17) if k == "udp64" else (1 << 15))
         ref1[k] = r1
         refA[k] = ref_harness_all_cores(CONFIGS[k]["cfg"], k, t16,
                                         r1.get("value") if isinstance(r1, dict) else None)
-    return {"value": round(tA, 3), "unit": "Mpkt/s", "cores": avail, "kind": "port",
+    port = {"value": round(tA, 3), "unit": "Mpkt/s", "cores": avail, "kind": "port",
             "sample": f"{key}: fields + PRINT_NORM text with frame header lines (the reference prints as "
                       f"it parses; `netsniff-ng --in`'s text) by the CPU "
                       f"restatement (oracle/nsd_oracle.c), {avail} threads (every available core) over "
                       f"contiguous shards, {pA} packets (passes over a resident "
-                      f"{max(1 << 20, 4096 * avail) if more else 1 << 20}-packet sample) in {dA:.1f} s",
+                      f"{max(1 << 20, 4096 * avail) if more else 1 << 20}-packet sample) in {dA:.1f} s"}
+    ref = refA.get(key)
+    if isinstance(ref, dict) and ref.get("value"):
+        head = {"value": ref["value"], "unit": "Mpkt/s", "cores": ref["cores"], "kind": "reference",
+                "sample": ref["sample"], "port": port}
+    else:
+        head = dict(port, reference_error=ref.get("error") if isinstance(ref, dict) else "oracle/_ref not built")
+    return dict(head, **{
             "cpu_model": model, "nproc": nproc, "cpus_available": avail, "cgroup_cpu_quota": cpu_quota(),
             "text_1thread": round(t1, 3),
             "text_16threads": {"threads": t16, "value": round(tS, 3)},
@@ -553,7 +600,7 @@ def cpu_baseline(key, seconds):
             "reference_harness_1thread": ref1.get(key, ref1["udp64"]),
             "reference_harness_1thread_by_workload": ref1,
             "reference_harness_all_cores": refA,
-            "reference_dissector_1thread": ref_harness_rate(cfg, key, frames=False)}
+            "reference_dissector_1thread": ref_harness_rate(cfg, key, frames=False)})
 
 
 # ---- host-memory legs (reported, never `value`) ----------------------------------------
@@ -606,12 +653,15 @@ def bpf_bench(b, steps, warmup):
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_pkt": round(algo / n, 2)}}
 
 
-def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
+def end_to_end(key, batch, nbatch, depth, mode, reps=3):
     """Host memory in, records in host memory out: `nbatch`
-    batches of `batch` packets from one pinned host buffer go through the
-    pipelined path (nsd_pipe_*, compact records: H2D, dissect kernels, D2H of
-    records, counters and - when a record needs them - side words / ext
-    entries, `depth` batches in flight)."""
+    batches of `batch` packets of config `key` from one pinned host buffer
+    go through the pipelined path (nsd_pipe_*, compact records: H2D, dissect
+    kernels, D2H of records, counters and - when a record needs them - side
+    words / ext entries, `depth` batches in flight).  The batches' summed
+    counters are checked against the oracle's for the same packets when the
+    run covers a whole golden shard (tests/golden/shard_counters.json)."""
+    cfg = CONFIGS[key]["cfg"]
     L = nsd.lib()
     n = batch * nbatch
     frames, desc = T.make_batch(cfg, n, lo=0, threads=16)
@@ -644,6 +694,10 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
             times.append(dt)
     pipe.close()
     assert int(cnts[:, nsd.CNT_PKTS].sum()) == n and not sts.any()
+    # every pass wrote the same counters; the last one's are checked
+    want = golden_counters(key, n, 1) if mode == nsd.PRINT_NORM else None
+    if want is not None:
+        assert np.array_equal(cnts.sum(axis=0, dtype=np.uint64), want), f"e2e {key}: counters differ from the oracle's"
     h2d = sum(f.nbytes - nsd.FRAME_PAD + d.nbytes for f, d, _ in slices)
     d2h = n * CREC_B
     dt = min(times)
@@ -652,8 +706,10 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
     for ok, (_, d, _) in zip(descs_pinned, slices):
         if ok:
             L.nsd_host_unregister(d.ctypes.data)
-    return {"value": round(n / dt / 1e6, 2), "unit": "Mpkt/s",
+    return {"workload": CONFIGS[key]["name"], "value": round(n / dt / 1e6, 2), "unit": "Mpkt/s",
             "pcie_gbs": round((h2d + d2h) / dt / 1e9, 2),
+            "counters_check": ("summed over the batches = the oracle's counters of the shard "
+                               "(tests/golden/shard_counters.json)") if want is not None else None,
             "h2d_bytes_per_pkt": round(h2d / n, 2), "d2h_bytes_per_pkt": CREC_B,
             "records": "compact 8 B (nsd_crec)",
             "batches": nbatch, "batch_packets": batch, "depth": depth,
@@ -662,12 +718,40 @@ def end_to_end(cfg, batch, nbatch, depth, mode, reps=3):
                     "(nsd_pipe_*, compact records), best of %d passes" % reps}
 
 
-def replay_leg(cfg, n, mode, threads, reps=2):
+PREFIX = os.path.join(ROOT, "tests", "golden", "prefix.json")
+
+
+def replay_digest(key, mode, threads):
+    """The replay's text checked: the first 65,536 records of config `key`
+    as a pcap replayed through the device (the timed leg's path, unwrapped
+    text) must hash to what the reference's own read_pcap loop printed for
+    the same file (nsref -f; tests/golden/prefix.json replay_text_sha256).
+    Returns the check's description (None: no golden for this mode)."""
+    if not os.path.exists(PREFIX):
+        return None
+    with open(PREFIX) as f:
+        want = json.load(f).get(f"{key}:m{mode}", {}).get("replay_text_sha256")
+    if want is None:
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "prefix.pcap")
+        T.synth().nsd_synth_pcap(CONFIGS[key]["cfg"], T.SEED, 0, 65536, path.encode())
+        got, text = nsd.replay_pcap(path, mode=mode, threads=threads)
+    assert got == 65536 and hashlib.sha256(text).hexdigest() == want, f"replay {key}: text differs from the reference's"
+    return ("sha256 of the replayed text of the first 65,536 records = the reference's own --in loop's "
+            "(nsref -f, tests/golden/prefix.json)")
+
+
+def replay_leg(key, n, mode, threads, reps=2):
     """`netsniff-ng --in file.pcap` through the device (nsd_replay_pcap): a
-    synthetic pcap of n records in a temp file -> reader -> pipelined device
-    walk (compact records) -> host formatter pool of `threads` threads ->
-    /dev/null; and the same with one formatter thread over n/8 records (the
-    product formatter's single-thread rate, beside cpu_baseline.text_1thread)."""
+    synthetic pcap of n records of config `key` in a temp file -> reader ->
+    pipelined device walk (compact records) -> host formatter pool of
+    `threads` threads -> /dev/null; and the same with one formatter thread
+    over n/8 records (the product formatter's single-thread rate, beside
+    cpu_baseline.text_1thread).  The text itself is checked by
+    replay_digest."""
+    cfg = CONFIGS[key]["cfg"]
+    check = replay_digest(key, mode, threads)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "replay.pcap")
         T.synth().nsd_synth_pcap(cfg, T.SEED, 0, n, path.encode())
@@ -690,8 +774,8 @@ def replay_leg(cfg, n, mode, threads, reps=2):
             best1 = best_of(path1, n1, 1)
         finally:
             os.close(fd)
-    return {"value": round(n / best / 1e6, 3), "unit": "Mpkt/s", "packets": n,
-            "file_gbs": round(size / best / 1e9, 2), "format_threads": threads,
+    return {"workload": CONFIGS[key]["name"], "value": round(n / best / 1e6, 3), "unit": "Mpkt/s", "packets": n,
+            "file_gbs": round(size / best / 1e9, 2), "format_threads": threads, "text_check": check,
             "format_1thread": round(n1 / best1 / 1e6, 3),
             "note": "pcap file -> nsd_pcap reader -> H2D -> dissect kernels -> D2H compact records -> "
                     "formatter pool -> writev /dev/null (nsd_replay_pcap), best of %d" % reps}
@@ -764,10 +848,13 @@ def measure_rank(args, rank, world, dev, engine="device"):
     per_rank = args.packets * args.shards
     lo, _ = nsd_dist.weak_shard(per_rank, rank)
     compact = args.records == "compact"
+    t_setup = time.perf_counter()   # the shard's generation and upload (the N-rank budget)
     if engine == "device":
         b = Batch(args.config, args.packets, lo, args.shards, dev, compact=compact)
+        torch.cuda.synchronize()
     else:
         b = HostBatch(args.config, args.packets, lo, args.shards, compact=compact)
+    t_setup = time.perf_counter() - t_setup
     multi = nsd_dist.initialized()
     warm(b, args.mode, args.warmup, args.grid,
          seconds=WARM_SECONDS if engine == "device" else 0.0,
@@ -799,13 +886,13 @@ def measure_rank(args, rank, world, dev, engine="device"):
     elapsed = time.perf_counter() - t0
     kern_ms = (evs[0][0].elapsed_time(evs[0][1]) / args.steps if accumulate
                else float(np.mean([a.elapsed_time(c) for a, c in evs])))
-    elapsed, kern_ms = nsd_dist.max_over_ranks([elapsed, kern_ms], dev)
+    elapsed, kern_ms, t_setup = nsd_dist.max_over_ranks([elapsed, kern_ms, t_setup], dev)
     cnt = b.counters.cpu().numpy().view(np.uint64).copy()
     total_pkts = b.n * world
     assert int(cnt[nsd.CNT_PKTS]) == total_pkts * (args.steps if accumulate else 1), "counter check failed"
     assert not accumulate or int(b.ext_used.item()) == 0, "ext pool used while accumulating"
     return b, {"elapsed": elapsed, "kern_ms": kern_ms, "counters": cnt, "total_pkts": total_pkts,
-               "accumulate": accumulate, "frame_bytes": b.frame_bytes}
+               "accumulate": accumulate, "frame_bytes": b.frame_bytes, "setup_s": t_setup}
 
 
 
@@ -857,6 +944,7 @@ def workload_result(args, key, b, m, world, engine, traffic=None, copy_gbs=None,
             "value": round(total * args.steps / elapsed / 1e6, 2), "unit": "Mpkt/s",
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "kernel_value": round(total / (kern_ms * 1e-3) / 1e6, 2),
+            "setup_s": round(m["setup_s"], 2),
             "gbps_frames": round(m["frame_bytes"] * world * args.steps / elapsed / 1e9, 1),
             "roofline": b.roofline(kern_ms, tr, copy_gbs, ceiling),
             "counters": nsd.unpack_counters(m["counters"]),
@@ -889,6 +977,10 @@ def parse_args(argv=None):
     ap.add_argument("--e2e-batches", type=int, default=16)
     ap.add_argument("--e2e-depth", type=int, default=3)
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    # the CPU tests' switch: every rank walks its shards with the product's
+    # host walk over gloo (tests/test_multi.py runs `bench.py --gpus 2` this
+    # way, through spawn_ranks and torch.distributed.run); never a bench run
+    ap.add_argument("--engine", default="device", choices=["device", "host"], help=argparse.SUPPRESS)
     ap.add_argument("--pmc-configs", default="", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -971,21 +1063,34 @@ def run(args, rank, world, dev, engine="device", traffic=None):
     if solo and dev_eng and not args.no_cpu:
         cpu = cpu_baseline(args.config, args.cpu_seconds)
 
+    # the host-memory legs for the headline workload and, beside it, IMIX
+    # (north_star: 64 B and IMIX), as "imix" keys of the headline's dicts
+    host_keys = [args.config] + (["imix"] if args.config != "imix" and not args.no_legs else [])
     e2e = None
     if solo and dev_eng and not args.no_e2e:
-        e2e = end_to_end(CONFIGS[args.config]["cfg"], args.e2e_batch, args.e2e_batches, args.e2e_depth, args.mode)
+        for k in host_keys:
+            r = end_to_end(k, args.e2e_batch, args.e2e_batches, args.e2e_depth, args.mode)
+            if e2e is None:
+                e2e = r
+            else:
+                e2e[k] = r
 
     replay = None
     if solo and dev_eng and not args.no_replay:
-        replay = replay_leg(CONFIGS[args.config]["cfg"], args.replay_packets, args.mode, min(cpu_info()[2], 16))
-        if cpu is not None:
-            # the CPU-only text rate on the same thread count
-            replay["cpu_text_same_threads"] = cpu["text_16threads"]["value"]
-            replay["vs_cpu_text_same_threads"] = round(replay["value"] / cpu["text_16threads"]["value"], 3)
-            ref = (cpu.get("reference_harness_all_cores") or {}).get(args.config)
+        for k in host_keys:
+            r = replay_leg(k, args.replay_packets, args.mode, min(cpu_info()[2], 16))
+            if cpu is not None and k == args.config:
+                # the CPU-only text rate on the same thread count
+                r["cpu_text_same_threads"] = cpu["text_16threads"]["value"]
+                r["vs_cpu_text_same_threads"] = round(r["value"] / cpu["text_16threads"]["value"], 3)
+            ref = ((cpu or {}).get("reference_harness_all_cores") or {}).get(k)
             if isinstance(ref, dict) and ref.get("value"):
-                replay["reference_same_cores"] = ref["value"]
-                replay["vs_reference_same_cores"] = round(replay["value"] / ref["value"], 2)
+                r["reference_same_cores"] = ref["value"]
+                r["vs_reference_same_cores"] = round(r["value"] / ref["value"], 2)
+            if replay is None:
+                replay = r
+            else:
+                replay[k] = r
 
     if rank != 0:
         return None
@@ -1003,6 +1108,7 @@ def run(args, rank, world, dev, engine="device", traffic=None):
         "roofline": roofline,
         "counters_total": int(m["counters"][nsd.CNT_PKTS]),
         "counters_check": head["counters_check"],
+        "setup_s": head["setup_s"],
         "legs": leg_out or None,
         "other_records": other,
         "cpu_baseline": cpu,
@@ -1017,17 +1123,19 @@ def run(args, rank, world, dev, engine="device", traffic=None):
 
 
 def main():
+    t_start = time.perf_counter()
     args = parse_args()
     if args.pmc_child:
         pmc_child(args)
         return
+    host = args.engine == "host"
 
     rank, world, local = nsd_dist.rank_env()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: start the N ranks here, as fresh processes; this one
         # never touches a GPU (the devices are counted in a child process)
         have = nsd_dist.count_devices()
-        if have < args.gpus:
+        if have < args.gpus and not host:
             print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible", file=sys.stderr)
             sys.exit(2)
         sys.exit(nsd_dist.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
@@ -1039,16 +1147,24 @@ def main():
 
     # PMC traffic first, in child processes, before this process initialises the GPU
     traffic = None
-    if solo and not args.no_pmc:
+    if solo and not args.no_pmc and not host:
         traffic = pmc_traffic(args, [args.config] + legs)
 
-    if world > 1:
+    if host:
+        if world > 1:
+            nsd_dist.init("gloo")
+        dev = torch.device("cpu")
+    elif world > 1:
         nsd_dist.init("nccl", local)
+        dev = torch.device("cuda", local)
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
-    out = run(args, rank, world, dev, "device", traffic)
+        dev = torch.device("cuda", 0)
+    out = run(args, rank, world, dev, args.engine, traffic)
     if out is not None:
+        # this process's wall time from start to the line (rank 0; the ranks
+        # meet at every workload's barriers, so it is the job's)
+        out["bench_wall_s"] = round(time.perf_counter() - t_start, 1)
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -174,6 +174,8 @@ enum nsd_counter {
 	NSD_CNT_EXT       = 37,  /* records using the ext pool */
 	NSD_CNT_OVERFLOW  = 38,  /* records flagged NSD_F_OVERFLOW */
 	NSD_CNT_TRIM      = 39,  /* IPv4 tail trims (tail_off < caplen) */
+	NSD_CNT_LISTOVF   = 40,  /* waves whose pending list overran its slots: a kernel
+	                            invariant broken, never expected (results unreliable) */
 	NSD_NCOUNTERS     = 64
 };
 
@@ -458,6 +460,13 @@ int nsd_last_schedule(void);
  * the default; tests use it to give small batches several tiles per wave).
  * Process-wide; returns the previous cap, or NSD_ERR_ARG. */
 int nsd_set_grid_cap(int blocks);
+/* nsd_set_record_ring: whether the fused kernel's compact records of tiles
+ * with deferred packets go through its per-wave record ring (coalesced
+ * stores once a tile is finished; results identical either way): 0
+ * adaptive (the default: on for batches whose schedule sample defers more
+ * than a quarter of the packets, and until the first sample), 1 on, 2 off.
+ * Process-wide (tests); returns the previous setting, or NSD_ERR_ARG. */
+int nsd_set_record_ring(int mode);
 
 /* Compact-record pipe: nsd_pipe_create_compact as nsd_pipe_create, its
  * batches walked into nsd_crec records.  The pool needs ext_words >=

@@ -77,6 +77,9 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #ifndef NSD_FAST_EXT
 #define NSD_FAST_EXT 1             // the fused kernel's fast walk steps extension headers in its window
 #endif
+#ifndef NSD_RING
+#define NSD_RING 1                 // the fused kernel's compact records through the per-wave record ring (RingSt)
+#endif
 #ifndef NSD_CSUM_SPLIT
 #define NSD_CSUM_SPLIT 1           // dissect_icmp blocks per pass-1 block
 #endif
@@ -475,54 +478,48 @@ __device__ __forceinline__ void store_rec(uint4 *rec, uint32_t i, uint4 r)
 // renderer re-derives from the bytes: the first 6 ids, the layer count in
 // nlayers for 7..12 layers (ids 6..11 in the packet's side word), or the ext
 // slot of a longer chain
+__device__ __forceinline__ uint2 crec_of(const WalkOut &w)
+{
+	const bool more = w.n > NSD_REC_MAX_LAYERS;
+	const uint32_t nf = (more ? NSD_N_EXT : w.n) | w.flags;
+	const uint32_t rs = more && !w.ext_on ? w.n : 0u;
+	return make_uint2(w.ext_on ? w.slot : w.chain, w.ip_csum | nf << 16 | rs << 24);
+}
+
 template <bool CR>
 __device__ __forceinline__ void put_rec(void *rec, uint32_t i, const WalkOut &w)
 {
 	if constexpr (CR) {
-		const bool more = w.n > NSD_REC_MAX_LAYERS;
-		const uint32_t nf = (more ? NSD_N_EXT : w.n) | w.flags;
-		const uint32_t rs = more && !w.ext_on ? w.n : 0u;
-		const v2u v = { w.ext_on ? w.slot : w.chain, w.ip_csum | nf << 16 | rs << 24 };
-		__builtin_nontemporal_store(v, (v2u *)rec + i);
+		const uint2 r = crec_of(w);
+		__builtin_nontemporal_store(v2u{ r.x, r.y }, (v2u *)rec + i);
 	} else {
 		store_rec((uint4 *)rec, i, pack_record(w));
 	}
 }
 
-// The fused tile loop's compact records and pending-list entries, held one
-// tile (the 16-byte form stores at once: held, they spill registers): a
-// tile's stores are issued after the next tile's chunk wait and before its
-// prefetch loads, so the wait that precedes each tile (vmcnt(0): its chunks
-// are the youngest loads) finds them issued a whole tile earlier (C3 -1 %).
-// (Nontemporal stores: as sc1 stores, the split kernel's choice below, C3
-// ran 1.5 % slower.)
-// Measured on the C3 tile phase without its walk: the record
-// stores cost 0.07 of its 0.35 ms however they are issued - every tile or
-// every fourth in 4x larger pieces, 8 or 16 bytes per lane, held or not -
-// i.e. the writes' interleaving with the scattered window reads in HBM, not
-// a wait in this loop.
+// The fused tile loop's pending-list entries and, without the record ring
+// (NSD_RING 0: r05's schedule), its compact records, held one tile: a
+// tile's stores are issued after the next tile's
+// chunk wait and before its prefetch loads, so the wait that precedes each
+// tile (vmcnt(0): its chunks are the youngest loads) finds them issued a
+// whole tile earlier (C3 -1 %).  (Nontemporal stores: as sc1 stores, the
+// split kernel's choice below, C3 ran 1.5 % slower.)  Measured on the C3
+// tile phase without its walk: the record stores cost 0.07
+// of its 0.35 ms however they are issued - every tile or every fourth in 4x
+// larger pieces, 8 or 16 bytes per lane, held or not - i.e. the writes'
+// interleaving with the scattered window reads in HBM, not a wait in this
+// loop.  The 16-byte form stores at once (held, its four words spill the
+// fused kernel's registers).
 template <bool CR>
 struct HeldSt {
-	uint2 r;          // the compact record (nsd_crec; 16-byte records are not held)
+	uint2 r;          // the compact record (nsd_crec)
 	uint32_t ri;      // packet index of the record; ~0: none
 	uint64_t pe;      // pending-list entry
 	uint32_t pp;      // its slot; ~0: none
-	__device__ __forceinline__ void hold_rec(void *rec, uint32_t i, const WalkOut &w, bool on)
+	__device__ __forceinline__ void hold_rec(uint32_t i, uint2 rv, bool on)
 	{
-		if constexpr (!CR) {
-			// (the 16-byte record is stored at once: held, its four words
-			// spill the fused kernel's registers)
-			if (on)
-				store_rec((uint4 *)rec, i, pack_record(w));
-			return;
-		}
 		ri = on ? i : 0xFFFFFFFFu;
-		if constexpr (CR) {
-			const bool more = w.n > NSD_REC_MAX_LAYERS;
-			const uint32_t nf = (more ? NSD_N_EXT : w.n) | w.flags;
-			const uint32_t rs = more && !w.ext_on ? w.n : 0u;
-			r = make_uint2(w.ext_on ? w.slot : w.chain, w.ip_csum | nf << 16 | rs << 24);
-		}
+		r = rv;
 	}
 	__device__ __forceinline__ void hold_pend(uint64_t *wq, uint64_t e, uint32_t slot)
 	{
@@ -598,10 +595,8 @@ __device__ __forceinline__ void put_rec_st(void *rec, uint32_t i, const WalkOut 
 	if (!NSD_FAST_ASMST) {
 		put_rec<CR>(rec, i, w);
 	} else if constexpr (CR) {
-		const bool more = w.n > NSD_REC_MAX_LAYERS;
-		const uint32_t nf = (more ? NSD_N_EXT : w.n) | w.flags;
-		const uint32_t rs = more && !w.ext_on ? w.n : 0u;
-		const v2u v = { w.ext_on ? w.slot : w.chain, w.ip_csum | nf << 16 | rs << 24 };
+		const uint2 r = crec_of(w);
+		const v2u v = { r.x, r.y };
 		asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"((v2u *)rec + i), "v"(v) : "memory");
 	} else {
 		const uint4 r = pack_record(w);
@@ -693,9 +688,130 @@ struct Shared {
 	uint32_t step[64];                          // c_step, c_lay2h (general walk)
 	uint32_t wc[WAVES][2];                      // per-wave ext pool chunk {next word, words left}
 	uint32_t pcnt[WAVES];                       // pending checksums per wave
-	uint32_t lay[WAVES][NSD_LDS_LAYERS * 64];   // general-walk layer lists (layers 6..15)
+	// general-walk layer lists (layers 6..11, 16-byte records); compact
+	// records keep no layer starts, and the fused kernel's waves use the
+	// words as their record rings (RecRing)
+	alignas(16) uint32_t lay[WAVES][NSD_LDS_LAYERS * 64];
 	uint8_t tmap[WAVES][64];                    // take(): pending lane of each rank
 };
+
+// The fused kernel's record ring (compact records).  A tile whose packets
+// the fast walk all finishes stores its records at once, right after its
+// fast walk (C3: the same time as r05's records held one tile in registers,
+// HeldSt, which no longer fit beside the ring's code: 11 VGPRs spilled,
+// C3 +28 %).  A tile with deferred packets has its records written
+// twice over: by the fast walk (the packets it finishes) and later by the
+// walkers' sessions (each session's finished packets), often across two
+// tiles.  Stored to HBM as they came, a 128-byte line of records (16
+// packets) was written in two or three pieces microseconds apart, and the
+// XCD's L2 had let the line go in between, so each piece cost its own
+// partial-line writes (C4: 17.4 B/packet written for 8 B of records, and
+// 6.3 more for the side words' 4-byte stores; TCC_EA0_WRREQ: 37 % of the
+// requests 32-byte ones).  Here each wave keeps two such tiles' records and
+// side words in LDS (the compact form's unused layer-list words: 2 x 64 x 8
+// B + 2 x 64 x 4 B = 1,536 B a wave) and stores a tile's records in one
+// coalesced wave store (512 B, whole lines) once its last packet is
+// finished; its side words likewise (256 B) when any packet of the tile has
+// one (C4), zero for the tile's packets without one.  A slot needed by a new
+// tile while packets of its old tile are still held by walkers (walked
+// across two more tiles) stores the finished ones at once, and those
+// walkers store theirs directly (the tile has left the ring).  The state is
+// wave-uniform and lives in scalar registers: a round trip to LDS for it
+// before each tile's prefetch loads cost C3 5 %.
+constexpr uint32_t RING_NONE = 0xFFFFFFFFu;
+struct RingSt {
+	// (scalars, never an array indexed at run time: that would go to scratch)
+	uint32_t tb0, tb1;       // the tile (first packet) of slot 0 / 1, RING_NONE: free
+	uint32_t left0, left1;   // its packets not yet finished
+	uint32_t any;            // bit s: a packet of slot s's tile has a side word
+	uint32_t next;           // the slot the next tile with deferrals takes
+	__device__ __forceinline__ void init()
+	{
+		tb0 = tb1 = RING_NONE;
+		left0 = left1 = any = next = 0;
+	}
+	__device__ __forceinline__ uint32_t tb(int s) const { return s ? tb1 : tb0; }
+	__device__ __forceinline__ uint32_t left(int s) const { return s ? left1 : left0; }
+	__device__ __forceinline__ void set(int s, uint32_t t, uint32_t l)
+	{
+		if (s) {
+			tb1 = t;
+			left1 = l;
+		} else {
+			tb0 = t;
+			left0 = l;
+		}
+	}
+};
+// this wave's slots (addresses recomputed at each use: nothing of them stays
+// live across the walker engine, whose registers are at their limit)
+__device__ __forceinline__ uint2 *ring_rec(Shared &sh)
+{
+	return (uint2 *)&sh.lay[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))][0];
+}
+__device__ __forceinline__ uint32_t *ring_side(Shared &sh)
+{
+	return &sh.lay[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))][256];
+}
+static_assert(NSD_LDS_LAYERS * 64 >= 2 * 64 * 2 + 2 * 64, "two tiles of compact records and side words");
+
+// Lanes with fin finished packet i with record r and side word sv (0:
+// none): into its tile's slot, or straight to HBM when the tile is not in
+// the ring.  Wave-uniform call.
+__device__ __forceinline__ void ring_put(Shared &sh, RingSt &rs, bool fin, uint32_t i, uint2 r, uint32_t sv,
+					 void *__restrict__ rec, uint32_t *__restrict__ side)
+{
+	const uint32_t tb = i & ~63u;
+	const int sl = !fin ? -1 : tb == rs.tb0 ? 0 : tb == rs.tb1 ? 1 : -1;
+	if (sl >= 0) {
+		ring_rec(sh)[sl * 64 + (i & 63)] = r;
+		ring_side(sh)[sl * 64 + (i & 63)] = sv;
+	} else if (fin) {
+		__builtin_nontemporal_store(v2u{ r.x, r.y }, (v2u *)rec + i);
+		if (sv)
+			side[i] = sv;
+	}
+	rs.left0 -= (uint32_t)__popcll(__ballot(sl == 0));
+	rs.left1 -= (uint32_t)__popcll(__ballot(sl == 1));
+	rs.any |= (__ballot(sl == 0 && sv != 0) ? 1u : 0u) | (__ballot(sl == 1 && sv != 0) ? 2u : 0u);
+}
+
+// Store slot s's tile - the records of its packets (lane k: packet tb + k;
+// `held`: still on a walker, not stored) in one wave store, its side words
+// in another when any is set - and free the slot.  Wave-uniform call.
+__device__ __forceinline__ void ring_store(Shared &sh, RingSt &rs, int s, bool held, void *__restrict__ rec,
+					   uint32_t *__restrict__ side, uint32_t n, int lane)
+{
+	wave_sync_lds();
+	const uint32_t i = rs.tb(s) + (uint32_t)lane;
+	const bool on = !held && i < n;
+	const uint2 r = ring_rec(sh)[s * 64 + lane];
+	if (on)
+		__builtin_nontemporal_store(v2u{ r.x, r.y }, (v2u *)rec + i);
+	if (rs.any & (1u << s)) {
+		const uint32_t sv = ring_side(sh)[s * 64 + lane];
+		if (on)
+			side[i] = sv;
+	}
+	wave_sync_lds();   // (the slot's next writes after these reads)
+	rs.set(s, RING_NONE, 0);
+	rs.any &= ~(1u << s);
+}
+
+// A tile with `nd` deferred packets (nd > 0) takes the next slot (free:
+// ring_turn) with the records of the packets the fast walk finished (`done`)
+__device__ __forceinline__ void ring_open(Shared &sh, RingSt &rs, uint32_t base, uint32_t nd, bool done, uint2 r,
+					  uint32_t sv, int lane)
+{
+	const int s = (int)rs.next;
+	if (done) {
+		ring_rec(sh)[s * 64 + lane] = r;
+		ring_side(sh)[s * 64 + lane] = sv;
+	}
+	rs.set(s, base, nd);
+	rs.any |= __ballot(done && sv != 0) ? 1u << s : 0u;
+	rs.next ^= 1u;
+}
 
 // The LINKTYPE_LINUX_SLL head (dissector_sll.c:39-82): pulls nothing; in
 // print_full the next ops come from the packet's sockaddr_ll (sll_next).
@@ -743,9 +859,10 @@ __device__ __forceinline__ uint64_t leaf_entry_c(uint32_t i, uint32_t start, uin
 // one coalesced 4-byte store instead of a pool entry, C4 -25 %); only
 // longer chains (entry taken at layer 12 by take_deep) write an entry, with
 // ids only.
-template <int MODE, bool CR>
-__device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, uint32_t caplen, const GenSink<CR> &g,
-					     void *__restrict__ rec, Pending &pq, FlagCnt &fc, int lane)
+template <int MODE, bool CR, bool RING>
+__device__ __forceinline__ void emit_general(Shared &sh, RingSt &rs, bool fin, WalkOut &w, uint32_t i,
+					     uint32_t caplen, const GenSink<CR> &g, void *__restrict__ rec, Pending &pq,
+					     FlagCnt &fc, int lane)
 {
 	// a host-rendered leaf's end is walked by the leaf pass: into the 16-byte
 	// record's cursor, or (compact records with side words) into the side
@@ -772,9 +889,10 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 	}
 	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
 	static_assert(DEEP == NSD_CREC_MAX_LAYERS, "side words hold the LDS-listed layers");
+	// (a 7..12-layer chain's side word: ids 6..11, never 0)
+	const bool sw = CR && fin && w.n > NSD_REC_MAX_LAYERS && !w.ext_on;
 	if constexpr (CR) {
-		const bool sw = fin && w.n > NSD_REC_MAX_LAYERS && !w.ext_on;
-		if (sw && g.side)
+		if (sw && g.side && !RING)
 			g.side[i] = w.offB;
 		if (sw && !g.side)
 			w.flags |= NSD_F_OVERFLOW;   // no side words: the pool is smaller than the batch
@@ -811,7 +929,9 @@ __device__ __forceinline__ void emit_general(bool fin, WalkOut &w, uint32_t i, u
 					*(uint4 *)(e + 4 + g0) = make_uint4(lv(g0), lv(g0 + 1), lv(g0 + 2), lv(g0 + 3));
 		}
 	}
-	if (fin)
+	if (CR && RING)
+		ring_put(sh, rs, fin, i, crec_of(w), sw && g.side ? w.offB : 0u, rec, g.side);
+	else if (fin)
 		put_rec<CR>(rec, i, w);
 	fc.add(w, caplen, fin);
 }
@@ -840,6 +960,33 @@ struct Walker {
 	bool have;        // holds a packet
 	bool stage;       // its window must be (re)staged before it steps again
 };
+
+// The ring at the point where the previous tile's held stores go out
+// (walk_tiles, before the next tile's loads): every tile whose packets are
+// all finished is stored, and the slot the next tile with deferrals takes,
+// if its tile still has packets on walkers (walked across two more tiles),
+// stores the finished ones and leaves the ring.
+__device__ __forceinline__ void ring_turn(Shared &sh, RingSt &rs, const Walker &wk, void *__restrict__ rec,
+					  uint32_t *__restrict__ side, uint32_t n, int lane)
+{
+#pragma unroll
+	for (int k = 0; k < 2; k++)
+		if (rs.tb(k) != RING_NONE && rs.left(k) == 0)
+			ring_store(sh, rs, k, false, rec, side, n, lane);
+	const int s = (int)rs.next;
+	if (rs.tb(s) != RING_NONE) {
+		// which of the tile's packets walkers hold: a byte per packet in the
+		// wave's take() map (free outside take)
+		const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+		sh.tmap[wv][lane] = 0;
+		wave_sync_lds();
+		if (wk.have && (wk.i & ~63u) == rs.tb(s))
+			sh.tmap[wv][wk.i & 63] = 1;
+		wave_sync_lds();
+		const bool held = sh.tmap[wv][lane] != 0;
+		ring_store(sh, rs, s, held, rec, side, n, lane);
+	}
+}
 
 // How much of a walker's window to stage (walkers()).  An HBM read costs
 // whole 128-byte lines, and a chain's later layers need only a few bytes
@@ -879,8 +1026,8 @@ template <bool CR>
 __device__ __forceinline__ void take(Shared &sh, Walker &wk, bool &pnd, const WalkOut &pw, uint32_t pi, uint64_t pd,
 				     int lane, int wv);
 
-template <int MODE, bool CR>
-__device__ __forceinline__ void walkers(Shared &sh, const uint8_t *__restrict__ frames, void *__restrict__ rec,
+template <int MODE, bool CR, bool RING>
+__device__ __forceinline__ void walkers(Shared &sh, RingSt &rs, const uint8_t *__restrict__ frames, void *__restrict__ rec,
 					const GenSink<CR> &g, Pending &pq, FlagCnt &fc, Walker &wk, bool &pnd,
 					const WalkOut &pw, uint32_t pi, uint64_t pd, bool drain)
 {
@@ -939,7 +1086,7 @@ __device__ __forceinline__ void walkers(Shared &sh, const uint8_t *__restrict__ 
 		}
 		wave_sync_lds();
 		const bool fin = wk.have && wk.w.id == 0;
-		emit_general<MODE, CR>(fin, wk.w, wk.i, caplen, g, rec, pq, fc, lane);
+		emit_general<MODE, CR, RING>(sh, rs, fin, wk.w, wk.i, caplen, g, rec, pq, fc, lane);
 		wk.have = wk.have && !fin;
 		wk.stage = susp;
 		if (!drain && !more)
@@ -994,136 +1141,9 @@ __device__ __forceinline__ void take(Shared &sh, Walker &wk, bool &pnd, const Wa
 	pnd = pnd && rp >= nf;
 }
 
-// plain_walk / plain4_walk map protocols 1 / 6 / 17 without the eth_lay3
+// plain_walk maps protocols 6 / 17 without the eth_lay3
 // lookup fast_walk makes: the table must agree
 constexpr uint8_t k_plain_lay3[256] = NSD_LAY3_TABLE;
-
-// The IMIX chains (PRINT_NORM, both schedules): Ethernet, at most one
-// 802.1Q tag, IPv4 without options, then TCP, UDP or ICMPv4, in a frame of
-// at least 38 bytes (every pull up to the IPv4 header succeeds and the header
-// lies in the window).  For such a packet fast_walk reads the tag, the IPv4
-// header, the total length (trim), the protocol and - for ICMPv4 - the
-// message (proto_icmpv4.c:34-51: whole post-trim message summed, inside the
-// window, or left to the checksum pass), and the chain ends after the L4
-// ops.  plain4_is / plain4_walk do the same from 9 row dwords read at once
-// (bytes 12..43 by byte funnel shifts, one LDS wait) instead of fast_walk's
-// chain of dependent byte reads and lookups; a tile takes this path when
-// every valid lane's packet qualifies (wave-uniform), and its per-ops counts
-// come from ballots.  The tag, ICMPv4 and TCP / UDP maps of eth_lay2 /
-// eth_lay3 are asserted below.
-#ifndef NSD_PLAIN4
-#define NSD_PLAIN4 0          // the fused kernel's tiles (r05: C3 within noise once its stores were held, C4 +2 %)
-#endif
-#ifndef NSD_PLAIN4_SPLIT
-#define NSD_PLAIN4_SPLIT 0    // the split fast kernel's tiles
-#endif
-static_assert(k_plain_lay3[1] == NSD_OPS_ICMPV4, "plain4_walk's protocol map differs from eth_lay3");
-struct Plain4 {
-	uint32_t E[6];   // bytes 12+v .. 35+v as little-endian dwords (v: the tag's 4 bytes, or 0)
-	bool vlan;
-};
-__device__ __forceinline__ Plain4 plain4_read(const LSrc<true, WIN1> &s)
-{
-	const uint32_t r = s.m + 12, j = r >> 2, sh = r & 3;   // j + 8 <= 14: inside the row
-	uint32_t W[9], D[8];
-#pragma unroll
-	for (int k = 0; k < 9; k++)
-		W[k] = s.dw(j + k);
-#pragma unroll
-	for (int k = 0; k < 8; k++)
-		D[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh);
-	Plain4 p;
-	p.vlan = (D[0] & 0xFFFF) == 0x0081u;   // ethertype 0x8100 at byte 12
-#pragma unroll
-	for (int k = 0; k < 6; k++)
-		p.E[k] = p.vlan ? D[k + 1] : D[k];
-	return p;
-}
-// the ethertype at byte 12 alone: a first test that costs a tile of other
-// traffic (C4's IPv6) two row reads instead of plain4_read's nine
-__device__ __forceinline__ bool plain4_may(const LSrc<true, WIN1> &s)
-{
-	const uint32_t r = s.m + 12, j = r >> 2;
-	const uint32_t t = __builtin_amdgcn_alignbyte(s.dw(j + 1), s.dw(j), r & 3) & 0xFFFF;
-	return t == 0x0008u || t == 0x0081u;
-}
-__device__ __forceinline__ bool plain4_ok(const Plain4 &p, uint32_t caplen)
-{
-	// type 0x0800 at 12 + v (the inner type behind a tag), version / IHL 0x45,
-	// protocol 1 / 6 / 17
-	const uint32_t proto = p.E[2] >> 24;
-	return caplen >= 38 && (p.E[0] & 0xFFFFFFu) == 0x450008u && (proto == 1 || proto == 6 || proto == 17);
-}
-template <bool FOLD>
-__device__ __forceinline__ void plain4_walk(const LSrc<true, WIN1> &s, const Plain4 &p, uint32_t caplen, WalkOut &w)
-{
-	const uint32_t v = p.vlan ? 4u : 0u;
-	const uint32_t d2 = 34 + v;   // the L4 header
-	// calc_csum over the 10 header words at 14 + v (csum.h:12-27)
-	uint32_t sum = (p.E[0] >> 16) + (p.E[5] & 0xFFFF);
-#pragma unroll
-	for (int k = 1; k < 5; k++)
-		sum = __builtin_amdgcn_sad_u16(p.E[k], 0u, sum);
-	sum = (sum >> 16) + (sum & 0xffff);
-	sum += sum >> 16;
-	w.ip_csum = (uint16_t)~sum;
-	// the total-length trim (proto_ipv4.c:170-177; ihl 5)
-	const int32_t x = (int32_t)__builtin_bswap16((uint16_t)p.E[1]) - 20;
-	if (x >= 0 && (uint32_t)x < caplen - d2)
-		w.tail = d2 + (uint32_t)x;
-	const uint32_t proto = p.E[2] >> 24;
-	const int l4 = proto == 6 ? NSD_OPS_TCP : proto == 17 ? NSD_OPS_UDP : NSD_OPS_ICMPV4;
-	w.chain = p.vlan ? NSD_OPS_ETHERNET | NSD_OPS_VLAN << 5 | NSD_OPS_IPV4 << 10 | (uint32_t)l4 << 15
-			 : NSD_OPS_ETHERNET | NSD_OPS_IPV4 << 5 | (uint32_t)l4 << 10;
-	w.offA = p.vlan ? (uint64_t)14 << 16 | (uint64_t)18 << 32 | (uint64_t)38 << 48
-			: (uint64_t)14 << 16 | (uint64_t)34 << 32;
-	w.n = p.vlan ? 4 : 3;
-	const uint32_t len = w.tail - d2, hl = proto == 6 ? 20u : 8u;
-	w.data = len >= hl ? d2 + hl : d2;
-	if (l4 == NSD_OPS_ICMPV4 && len >= 8) {
-		// proto_icmpv4.c:42: calc_csum(icmp, pkt_len + 8) over the message
-		if (!s.in_window(d2, len & ~1u)) {
-			w.icmp_pend = true;
-			w.icmp_off = d2;
-			w.icmp_len = len;
-			if (FOLD) {
-				const uint32_t kw = s.window_bytes(d2) >> 1;
-				w.icmp_sum = s.sum16(d2, kw);
-				w.icmp_off = d2 + 2 * kw;
-				w.icmp_len = (len & ~1u) - 2 * kw;
-			}
-		} else if (calc_csum(s, d2, len >> 1)) {
-			w.flags |= NSD_F_ICMP_BAD;
-		}
-	}
-}
-// a plain4 tile's per-ops counts and flag counts from ballots (no host leaf,
-// ext chain, overflow or deferral in such a tile)
-__device__ __forceinline__ void plain4_count(uint32_t *s_ops, FlagCnt &fc, const WalkOut &w, bool valid,
-					     uint32_t caplen, int lane)
-{
-	const int l4 = (int)((w.chain >> (w.n == 4 ? 15 : 10)) & 31);
-	const uint32_t nv = FlagCnt::pc(valid), ng = FlagCnt::pc(valid && w.n == 4);
-	const uint32_t nt = FlagCnt::pc(valid && l4 == NSD_OPS_TCP), nu = FlagCnt::pc(valid && l4 == NSD_OPS_UDP);
-	if (lane == 0) {
-		atomicAdd(&s_ops[NSD_OPS_ETHERNET], nv);
-		atomicAdd(&s_ops[NSD_OPS_IPV4], nv);
-		if (ng)
-			atomicAdd(&s_ops[NSD_OPS_VLAN], ng);
-		if (nt)
-			atomicAdd(&s_ops[NSD_OPS_TCP], nt);
-		if (nu)
-			atomicAdd(&s_ops[NSD_OPS_UDP], nu);
-		if (nv - nt - nu)
-			atomicAdd(&s_ops[NSD_OPS_ICMPV4], nv - nt - nu);
-	}
-	fc.pkts += nv;
-	fc.ipbad += FlagCnt::pc(valid && w.ip_csum != 0);
-	fc.icmpbad += FlagCnt::pc(valid && (w.flags & NSD_F_ICMP_BAD));
-	fc.trim += FlagCnt::pc(valid && w.tail < caplen);
-	if (valid)
-		fc.bytes += caplen;
-}
 
 // ---- pending ICMPv4 checksums -------------------------------------------------
 // Runs after both passes (the records are final): the block's waves take its
@@ -1361,13 +1381,18 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	bool late = false;
 	HeldSt<CR> hs;   // the previous tile's record / pending-list stores
 	hs.ri = hs.pp = 0xFFFFFFFFu;
+	// compact records: the wave's record ring (RecRing), slot rs for the
+	// next tile
+	constexpr bool RG = CR && NSD_RING;
+	RingSt rs;
+	rs.init();
 	// (one more pass after the last tile drains the walkers: the engine is
 	// inlined once)
 	// this wave's even share of tiles and the ones walked, for prio_level
 	const uint32_t share = (ntiles + nw - 1) / nw;
 	uint32_t done = 0, lvl = 0xFFu;
 	for (;;) {
-		if (NSD_PRIO && CR && prio) {   // (the 16-byte form's walk state leaves no registers for it)
+		if (NSD_PRIO && CR && (prio & 1)) {   // (the 16-byte form's walk state leaves no registers for it)
 			const uint32_t l = done < share ? 4u * done / share : 3u;
 			if (l != lvl) {
 				lvl = l;
@@ -1387,6 +1412,8 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 		if (!last) {
 			stage_write(&s_win[wv][0], ch, lane);
 			hs.flush(rec, wq);   // tile t-1's stores, before tile t+1's loads
+			if (RG)
+				ring_turn(sh, rs, wk, rec, g.side, n, lane);
 			// prefetch: descriptors of tile t+2, chunks of tile t+1
 			if constexpr (DYN) {
 				nb2 = take();
@@ -1403,16 +1430,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			uint32_t fw = FW_DONE;
 			const LSrc<true, WIN1> src{ &s_win[wv][lane * ROW], s_lay3, nullptr, frames + off, caplen,
 						    (uint32_t)off & 15, 0, false };
-			// a tile of IMIX chains only: the straight-line walk (plain4_walk)
-			bool p4 = false;
-			if (NSD_PLAIN4 && MODE == PRINT_NORM && start_id == NSD_OPS_ETHERNET &&
-			    __ballot(valid && !plain4_may(src)) == 0) {
-				const Plain4 pr = plain4_read(src);
-				p4 = __ballot(valid && !plain4_ok(pr, caplen)) == 0;
-				if (p4 && valid)
-					plain4_walk<false>(src, pr, caplen, w);
-			}
-			if (!p4 && valid)
+			if (valid)
 				fw = fast_walk<MODE, false, NSD_FAST_EXT != 0>(src, caplen, w);
 			deferred = fw != FW_DONE;
 			ndefer += FlagCnt::pc(deferred);
@@ -1430,12 +1448,8 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			// per-ops counts from the finished chains, grouped by chain word
 			// (ids are >= 1, so equal chain words imply equal layer counts) for
 			// the first two distinct chains of the tile (C2: one), the rest per
-			// lane (C3: -4.5 % against looping over every distinct chain); a
-			// plain4 tile's from ballots
-			if (p4) {
-				plain4_count(sh.ops, fc, w, valid, caplen, lane);
-				hs.hold_rec(rec, i, w, valid);
-			} else {
+			// lane (C3: -4.5 % against looping over every distinct chain)
+			{
 				uint32_t key = done ? w.chain : 0xFFFFFFFFu;
 				for (int it = 0;; it++) {
 					const uint64_t pm = __ballot(key != 0xFFFFFFFFu);
@@ -1460,14 +1474,25 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 					if (key == lk)
 						key = 0xFFFFFFFFu;
 				}
-			if (CR && g.side && done && (w.flags & NSD_F_HOST)) {
-				// a leaf the fast walk finished (ARP, DCCP): its end in the side word
-				g.side[i] = w.data;
+			}
+			// a leaf the fast walk finished (ARP, DCCP): its end in the side word
+			const bool lend = CR && g.side && done && (w.flags & NSD_F_HOST);
+			if (lend)
 				w.flags |= NSD_F_LEAF_END;
+			const uint32_t nd = (uint32_t)__popcll(__ballot(deferred));
+			if (RG && (prio & 2) && nd) {
+				ring_open(sh, rs, base, nd, done, crec_of(w), lend ? w.data : 0u, lane);
+			} else if (CR && !RG) {
+				if (lend)
+					g.side[i] = w.data;
+				hs.hold_rec(i, crec_of(w), done);
+			} else {
+				if (lend)
+					g.side[i] = w.data;
+				if (done)
+					put_rec<CR>(rec, i, w);
 			}
-			hs.hold_rec(rec, i, w, done);
 			fc.add(w, caplen, done);
-			}
 			// the deferred packets' walk state for the general walk: from the
 			// start (FW_RESTART: other link types, MPLS, deeper tag stacks, bytes
 			// past the first window) or from where the fast walk stopped
@@ -1492,10 +1517,12 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			// (the walkers wait for their windows anyway: the held stores go
 			// first, and nothing is held across the engine's registers)
 			hs.flush(rec, wq);
-			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, pnd, w, i, d0, last);
+			walkers<MODE, CR, RG>(sh, rs, frames, rec, g, pq, fc, wk, pnd, w, i, d0, last);
 		}
 		if (last) {
 			hs.flush(rec, wq);
+			if (RG)
+				ring_turn(sh, rs, wk, rec, g.side, n, lane);   // every walker is done: the ring's last tiles
 			break;
 		}
 		// After a walker-heavy tile (C4) the next tile's chunks load here, with
@@ -1528,7 +1555,15 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			base += stride;
 		}
 	}
+	if (NSD_PRIO && CR && (prio & 1))
+		__builtin_amdgcn_s_setprio(0);   // the leaf and checksum passes at the neutral level
 	fc.flush(s_cnt, lane);
+	// the pending list held every entry (ask()'s room rule: a packet adds at
+	// most one, ICMPv4 from the front or leaf from the back, and the lists
+	// hold two shares plus four tiles); a broken invariant overwrote the next
+	// wave's list: counted, and the counters then differ from any oracle's
+	if (lane == 0 && pq.npend + pq.nleaf > pq.wcap)
+		atomicAdd(&s_cnt[NSD_CNT_LISTOVF], 1ull);
 	// the schedule sample (a launch the launcher samples passes its pair)
 	if (sched && lane == 0 && ndefer)
 		atomicAdd(&sched[0], (unsigned long long)ndefer);
@@ -1844,21 +1879,11 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 		// (every lane's row is staged, a lane past the batch from the clamped descriptor)
 		const bool plain = MODE == PRINT_NORM && start_id == NSD_OPS_ETHERNET &&
 				   __ballot(valid && !plain_is(src, caplen)) == 0;
-		bool p4 = false;
 		if (plain) {
 			if (valid)
 				plain_walk(src, caplen, w);
-		} else {
-			// a tile of IMIX chains only: the straight-line walk (plain4_walk)
-			if (NSD_PLAIN4_SPLIT && MODE == PRINT_NORM && start_id == NSD_OPS_ETHERNET &&
-			    __ballot(valid && !plain4_may(src)) == 0) {
-				const Plain4 pr = plain4_read(src);
-				p4 = __ballot(valid && !plain4_ok(pr, caplen)) == 0;
-				if (p4 && valid)
-					plain4_walk<true>(src, pr, caplen, w);
-			}
-			if (!p4 && valid)
-				fw = fast_walk<MODE, true>(src, caplen, w);
+		} else if (valid) {
+			fw = fast_walk<MODE, true>(src, caplen, w);
 		}
 		const bool deferred = fw != FW_DONE;
 		wave_sync_lds();
@@ -1899,13 +1924,7 @@ __device__ __forceinline__ void fast_tiles(FastShared &sh, const uint8_t *__rest
 			nicmp += (uint32_t)__popcll(pm);
 		}
 		// per-ops counts of the finished chains, grouped by chain word (as
-		// walk_tiles); a plain4 tile's from ballots
-		if (p4) {
-			plain4_count(sh.ops, fc, w, valid, caplen, lane);
-			if (valid)
-				put_rec_st<CR>(rec, i, w);
-			return;
-		}
+		// walk_tiles)
 		{
 			uint32_t key = done ? w.chain : 0xFFFFFFFFu;
 			for (int it = 0;; it++) {
@@ -2212,6 +2231,8 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
 	wk.stage = false;
 	WalkOut pw;
 	walk_init(pw, 0, 0);
+	RingSt rs;   // (unused: the walker kernel stores its records at once)
+	rs.init();
 
 	// chunk positions (wave-uniform): list L, first entry k0, the list's count
 	struct Pos {
@@ -2274,7 +2295,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
 				  (uint64_t)((c1.z >> 16) & 0xFF) << 48;
 			pw.offB = c1.z >> 24;
 		}
-		walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, pnd, pw, pi, pd, false);
+		walkers<MODE, CR, false>(sh, rs, frames, rec, g, pq, fc, wk, pnd, pw, pi, pd, false);
 		c0 = n0;
 		c1 = n1;
 		n0 = m0;
@@ -2285,7 +2306,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
 	{
 		bool none = false;
 		if (__ballot(wk.have))
-			walkers<MODE, CR>(sh, frames, rec, g, pq, fc, wk, none, pw, 0, 0, true);
+			walkers<MODE, CR, false>(sh, rs, frames, rec, g, pq, fc, wk, none, pw, 0, 0, true);
 	}
 	fc.flush(sh.cnt, lane);
 	leaf_pass<MODE, CR>(frames, desc, rec, ext, pq);
@@ -2316,6 +2337,12 @@ static uint32_t region_for(uint32_t n, uint32_t blocks)
 // group's tiles at run time (walk_tiles, compact records), so each list holds twice a wave's
 // even share plus four tiles (8 bytes a slot: within the workspace's first
 // 32 bytes per region slot, sched_pair_at)
+// (Each packet a wave visits adds at most one pending-list entry - an ICMPv4
+// message past its windows from the front, or a host-rendered leaf from the
+// back, never both: a leaf ends a chain that has no ICMPv4 layer - and
+// walk_tiles asks for a tile only while the list has room for every packet
+// of the tiles it holds; a wave that found its list overrun counts it in
+// NSD_CNT_LISTOVF.)
 static uint32_t region_for_fused(uint32_t n, uint32_t blocks, bool compact)
 {
 	return NSD_GROUP_TILES && compact ? 2 * region_for(n, blocks) + nsd::WAVES * 4 * 64 : region_for(n, blocks);
@@ -2358,7 +2385,9 @@ static size_t region_slots(uint32_t n)
 // box, where IMIX frames need the third: 0.78 against 0.92 ms); and when
 // more than a quarter of its packets went to the walkers, the fused kernel
 // runs without the progress priority (walk_tiles: C4 -1 % without it, C3
-// +0.7 %, in the same kernel).  State is per device.
+// +0.7 %, in the same kernel) and with the record ring (RingSt: C4's writes
+// halved, C3 +3 % with it; on until the first sample is read).  State is per
+// device.
 #ifndef NSD_SCHED_SAMPLE
 #define NSD_SCHED_SAMPLE 32
 #endif
@@ -2373,7 +2402,9 @@ constexpr int MAX_DEV = 16;
 struct Sched {
 	bool init = false, fused = false, pending = false, small = false;
 	bool walky = false;                    // the sample's deferred share above 25 % (no progress priority)
+	bool sampled_once = false;             // a sample has been read
 	bool recorded = false;                 // the pending sample's event is recorded (sched_sampled)
+	bool discard = false;                  // the pending sample failed: wait for its copies, use nothing
 	int launches = 0, last = 0;
 	uint64_t sampled = 0;                  // packets of the sampled launch in flight
 	unsigned long long *host = nullptr;    // its pair, then its counters [32, 34) before and after
@@ -2383,6 +2414,7 @@ struct Sched {
 Sched g_sched[MAX_DEV];
 std::mutex g_sched_mu;
 int g_sched_force = 0;   // 0 adaptive, NSD_SCHED_SPLIT, NSD_SCHED_FUSED
+int g_ring_force = 0;    // nsd_set_record_ring: 0 adaptive, 1 on, 2 off
 std::atomic<int> g_grid_cap{ 0 };   // nsd_set_grid_cap
 
 int cur_dev()
@@ -2397,7 +2429,7 @@ int cur_dev()
 // and whether this launch is the sample (then its pair is zeroed on
 // `stream` here and copied back by sched_sampled after the kernels).
 struct Plan {
-	bool fused, sample, small, prio;
+	bool fused, sample, small, prio, ring;
 	int cus;
 };
 Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, hipStream_t stream)
@@ -2411,7 +2443,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 			cus = 256;
 		S.cus = cus;
 	}
-	Plan p{ false, false, false, true, S.cus };
+	Plan p{ false, false, false, true, true, S.cus };
 	// a launch captured into a graph takes the schedule as it stands and is
 	// never the sample (an event query or a host copy would break the
 	// capture; the graph replays this plan)
@@ -2420,7 +2452,9 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 	// (a sample is read only once sched_sampled has recorded its event: between
 	// the plan and that record, the event still stands for an older sample, and
 	// another stream's launch must not take the copies in flight for it)
-	if (!capturing && S.pending && S.recorded && hipEventQuery(S.ev) == hipSuccess) {
+	if (!capturing && S.pending && S.recorded && hipEventQuery(S.ev) == hipSuccess && S.discard) {
+		S.pending = S.recorded = S.discard = false;
+	} else if (!capturing && S.pending && S.recorded && hipEventQuery(S.ev) == hipSuccess) {
 		const double rd = S.sampled ? (double)S.host[0] / (double)S.sampled : 0.0;
 		const double ri = S.sampled ? (double)S.host[1] / (double)S.sampled : 0.0;
 		S.fused = S.fused ? rd > 0.05 || ri > 0.05 : rd > 0.15 || ri > 0.10;
@@ -2428,6 +2462,7 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 		if (pk)
 			S.small = by <= (uint64_t)NSD_SMALL_FRAME * pk;
 		S.walky = rd > 0.25;
+		S.sampled_once = true;
 		S.pending = false;
 		S.recorded = false;
 	}
@@ -2440,6 +2475,9 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 	p.fused = g_sched_force ? g_sched_force == NSD_SCHED_FUSED : S.fused;
 	p.small = S.small;
 	p.prio = !S.walky;
+	// the record ring until a sample shows a quarter or less of the packets
+	// deferred (C3: +3 % with it; C4: writes 23.7 -> 12.2 B/packet)
+	p.ring = g_ring_force ? g_ring_force == 1 : !S.sampled_once || S.walky;
 	if (!capturing && ++S.launches >= NSD_SCHED_SAMPLE && !S.pending && S.host && pair && counters &&
 	    hipMemsetAsync(pair, 0, 16, stream) == hipSuccess &&
 	    hipMemcpyAsync(S.host + 2, counters + NSD_CNT_PKTS, 16, hipMemcpyDeviceToHost, stream) == hipSuccess) {
@@ -2453,6 +2491,22 @@ Plan sched_plan(uint32_t n, unsigned long long *pair, const uint64_t *counters, 
 	return p;
 }
 
+// A failed sample (under the lock): copies queued for it may still be in
+// flight into S.host, so the sample stays pending - no later sample queues
+// copies into the same words - until an event behind them completes, and
+// its values are discarded then (sched_plan).  Without an event, the stream
+// is drained here instead.
+void sched_fail(Sched &S, hipStream_t stream)
+{
+	S.discard = true;
+	if (hipEventRecord(S.ev, stream) == hipSuccess) {
+		S.recorded = true;
+		return;
+	}
+	(void)hipStreamSynchronize(stream);
+	S.pending = S.recorded = S.discard = false;
+}
+
 // after the sampled launch's kernels on `stream`: bring its pair and
 // counters back
 void sched_sampled(unsigned long long *pair, const uint64_t *counters, hipStream_t stream)
@@ -2462,20 +2516,18 @@ void sched_sampled(unsigned long long *pair, const uint64_t *counters, hipStream
 	if (hipMemcpyAsync(S.host, pair, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
 	    hipMemcpyAsync(S.host + 4, counters + NSD_CNT_PKTS, 16, hipMemcpyDeviceToHost, stream) != hipSuccess ||
 	    hipEventRecord(S.ev, stream) != hipSuccess) {
-		S.pending = false;   // no sample this time (the copies may still land: nothing reads them)
-		S.recorded = false;
+		sched_fail(S, stream);
 		return;
 	}
 	S.recorded = true;
 }
 
-// the sampled launch's kernels failed to launch: drop the sample
-void sched_abort()
+// the sampled launch's kernels failed to launch: drop the sample (once the
+// copies sched_plan queued for it have landed)
+void sched_abort(hipStream_t stream)
 {
 	std::lock_guard<std::mutex> g(g_sched_mu);
-	Sched &S = g_sched[cur_dev()];
-	S.pending = false;
-	S.recorded = false;
+	sched_fail(g_sched[cur_dev()], stream);
 }
 } // namespace
 
@@ -2486,6 +2538,16 @@ extern "C" int nsd_set_schedule(int sched)
 	std::lock_guard<std::mutex> g(g_sched_mu);
 	const int prev = g_sched_force;
 	g_sched_force = sched;
+	return prev;
+}
+
+extern "C" int nsd_set_record_ring(int mode)
+{
+	if (mode < 0 || mode > 2)
+		return NSD_ERR_ARG;
+	std::lock_guard<std::mutex> g(g_sched_mu);
+	const int prev = g_ring_force;
+	g_ring_force = mode;
 	return prev;
 }
 
@@ -2614,16 +2676,17 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 		hipLaunchKernelGGL(zero_tiles, dim3((blocks + 255) / 256), dim3(256), 0, stream, gtiles, blocks);
 		if (hipGetLastError() != hipSuccess) {
 			if (sched)
-				sched_abort();
+				sched_abort(stream);
 			return -2;
 		}
 	}
 	hipLaunchKernelGGL(f, dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec, d_ext,
 			   ext_words, d_ext_used, chunk_for(blocks), (unsigned long long *)d_counters, (uint64_t *)d_ws,
-			   region_for_fused(n, blocks, compact), (const uint32_t *)d_sll, sched, gtiles, plan.prio ? 1u : 0u);
+			   region_for_fused(n, blocks, compact), (const uint32_t *)d_sll, sched, gtiles,
+			   (plan.prio ? 1u : 0u) | (plan.ring ? 2u : 0u));
 	if (hipGetLastError() != hipSuccess) {
 		if (sched)
-			sched_abort();
+			sched_abort(stream);
 		return -2;
 	}
 	if (sched)
@@ -2669,7 +2732,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll, side, sched);
 	if (hipGetLastError() != hipSuccess) {
 		if (sched)
-			sched_abort();
+			sched_abort(stream);
 		return -2;
 	}
 	if (mi == 2)
@@ -2687,7 +2750,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 			   nlists, pend, per_wave * cap * WAVES);
 	if (hipGetLastError() != hipSuccess) {
 		if (sched)
-			sched_abort();
+			sched_abort(stream);
 		return -2;
 	}
 	if (sched)

@@ -19,6 +19,7 @@ LINKTYPE_EN10MB = 1
 NCOUNTERS = 64
 NSD_OPS_COUNT = 28
 CNT_PKTS, CNT_BYTES, CNT_IP_BAD, CNT_ICMP_BAD, CNT_HOST, CNT_EXT, CNT_OVERFLOW, CNT_TRIM = range(32, 40)
+CNT_LISTOVF = 40   # pending-list overruns (a broken kernel invariant; never expected)
 FRAME_PAD = 64
 F_ICMP_BAD, F_HOST, F_OVERFLOW, F_LEAF_END = 0x08, 0x10, 0x20, 0x40
 
@@ -36,6 +37,51 @@ EXT_MAX_LAYERS = 64
 
 # struct sock_filter (linux/filter.h) = nsd_bpf_insn
 BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])
+
+
+def source_hash():
+    """First 16 hex digits of the SHA-256 of the library's sources as they lie
+    in this tree: the sorted csrc/* files, the Makefile and the ABI header,
+    concatenated (the Makefile's SRCHASH, which it compiles into
+    nsd_build_info)."""
+    import glob
+    import hashlib
+    csrc = sorted(glob.glob(os.path.join(HERE, "csrc", "*")), key=lambda p: os.path.basename(p).encode())
+    files = [p for p in csrc if os.path.isfile(p)] + [os.path.join(HERE, "Makefile"),
+                                                      os.path.join(HERE, "..", "include", "netsniff_dissect.h")]
+    h = hashlib.sha256()
+    for p in files:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def built_source_hash(path=None):
+    """The source hash compiled into a built library (read from the file, not
+    loaded), or None when it has none or is missing."""
+    import re
+    try:
+        with open(path or LIB_PATH, "rb") as f:
+            m = re.search(rb"; sources ([0-9a-f]{16})", f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def ensure_built(jobs=8):
+    """Build the library in-tree when it is missing or its embedded source
+    hash is not the tree's (make by timestamps first; a full rebuild if the
+    hash still differs, e.g. a copied tree with older mtimes)."""
+    import subprocess
+    want = source_hash()
+    if built_source_hash() != want:
+        subprocess.run(["make", "-s", f"-j{jobs}", "-C", HERE], check=True)
+    if built_source_hash() != want:
+        subprocess.run(["make", "-s", "-B", f"-j{jobs}", "-C", HERE], check=True)
+    got = built_source_hash()
+    if got != want:
+        raise RuntimeError(f"libnsdissect.so carries sources {got}, the tree is {want}")
+    return got
 
 
 def ext_words(nlayers):
@@ -79,7 +125,8 @@ ABI_SYMBOLS = ["dissector_init_all", "dissector_entry_point", "dissector_cleanup
                "nsd_dissect_device_compact", "nsd_format_batch_compact", "nsd_pipe_create_compact",
                "nsd_pipe_submit_compact", "nsd_format_range_compact", "nsd_set_schedule",
                "nsd_last_schedule", "nsd_format_frame_hdr", "nsd_format_range_compact_fh",
-               "nsd_pcap_read_batch_fh", "nsd_t3_block_desc_fh", "nsd_pcap_index", "nsd_set_grid_cap"]
+               "nsd_pcap_read_batch_fh", "nsd_t3_block_desc_fh", "nsd_pcap_index", "nsd_set_grid_cap",
+               "nsd_set_record_ring"]
 
 # struct sockaddr_ll (nsd_sll_t), one per packet for LINKTYPE_LINUX_SLL batches
 SLL_DTYPE = np.dtype([("family", "<u2"), ("protocol", ">u2"), ("ifindex", "<i4"), ("hatype", "<u2"),
@@ -239,6 +286,18 @@ def set_schedule(sched):
     rc = lib().nsd_set_schedule(sched)
     if rc < 0:
         raise ValueError(f"bad schedule {sched}")
+    return rc
+
+
+RING_ADAPTIVE, RING_ON, RING_OFF = 0, 1, 2
+
+
+def set_record_ring(mode):
+    """The fused kernel's record ring: RING_ADAPTIVE (default), RING_ON or
+    RING_OFF; returns the previous setting (nsd_set_record_ring, tests)."""
+    rc = lib().nsd_set_record_ring(mode)
+    if rc < 0:
+        raise ValueError(f"bad record ring mode {mode}")
     return rc
 
 
@@ -564,6 +623,8 @@ def unpack_counters(counters):
                     ("icmp_bad", CNT_ICMP_BAD), ("host", CNT_HOST), ("ext", CNT_EXT),
                     ("overflow", CNT_OVERFLOW), ("trim", CNT_TRIM)]:
         out[name] = int(c[k])
+    if c[CNT_LISTOVF]:
+        out["list_overrun"] = int(c[CNT_LISTOVF])
     return out
 
 

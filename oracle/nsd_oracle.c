@@ -2353,3 +2353,79 @@ uint64_t nsor_dissect_batch_mt(const uint8_t *frames, const nsd_desc_t *desc, ui
 	free(jobs);
 	return sw;
 }
+
+/* The line floor of a batch (TEST / MEASUREMENT INFRASTRUCTURE, bench.py's
+ * roofline): the distinct 128-byte lines of the frame buffer that hold the
+ * bytes the chain must inspect, [off, off + W(pkt)) per packet (W as
+ * nsor_dissect's w_bytes: the algorithmic read extent).  An HBM read moves
+ * whole 128-byte lines, so no schedule that reads each needed line once can
+ * fetch less: the floor the measured traffic is compared with (plus 8 bytes
+ * of descriptor per packet).  Packets in order of offset (the synthetic
+ * batches); each thread walks a contiguous range, and a line two ranges
+ * share is counted once. */
+typedef struct {
+	const uint8_t *frames;
+	const nsd_desc_t *desc;
+	uint32_t lo, hi;
+	int linktype, mode;
+	uint64_t lines, first, last;   /* distinct lines; the range's first and last line (UINT64_MAX: none) */
+} lf_job;
+
+static void *lf_worker(void *arg)
+{
+	lf_job *j = arg;
+	nsor_info in;
+	nsd_rec r;
+	uint64_t last = UINT64_MAX;
+	j->first = UINT64_MAX;
+	for (uint32_t i = j->lo; i < j->hi; i++) {
+		const uint64_t d = j->desc[i], off = NSD_DESC_OFF(d);
+		nsor_dissect(j->frames + off, NSD_DESC_CAPLEN(d), j->linktype, j->mode, NULL, &r, &in);
+		if (!in.w_bytes)
+			continue;
+		uint64_t a = off >> 7;
+		const uint64_t b = (off + in.w_bytes - 1) >> 7;
+		if (j->first == UINT64_MAX)
+			j->first = a;
+		if (last != UINT64_MAX && a <= last)
+			a = last + 1;
+		if (b >= a)
+			j->lines += b - a + 1;
+		if (last == UINT64_MAX || b > last)
+			last = b;
+	}
+	j->last = last;
+	return NULL;
+}
+
+uint64_t nsor_line_floor_mt(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n, int linktype, int mode,
+			    int nthreads)
+{
+	pthread_t th[256];
+	lf_job *jobs;
+	uint64_t lines = 0, prev_last = UINT64_MAX;
+
+	if (nthreads < 1) nthreads = 1;
+	if (nthreads > 256) nthreads = 256;
+	jobs = calloc(nthreads, sizeof(*jobs));
+	for (int t = 0; t < nthreads; t++) {
+		jobs[t].frames = frames;
+		jobs[t].desc = desc;
+		jobs[t].lo = (uint32_t)((uint64_t)n * t / nthreads);
+		jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+		jobs[t].linktype = linktype;
+		jobs[t].mode = mode;
+		pthread_create(&th[t], NULL, lf_worker, &jobs[t]);
+	}
+	for (int t = 0; t < nthreads; t++) {
+		pthread_join(th[t], NULL);
+		lines += jobs[t].lines;
+		if (jobs[t].first != UINT64_MAX && jobs[t].first == prev_last)
+			lines--;   /* the line the previous range ended in */
+		if (jobs[t].last != UINT64_MAX)
+			prev_last = jobs[t].last;
+	}
+	free(jobs);
+	return lines;
+}
+

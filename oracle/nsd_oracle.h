@@ -73,6 +73,11 @@ uint64_t nsor_dissect_batch_text(const uint8_t *frames, const nsd_desc_t *desc,
 				 uint32_t n, int linktype, int mode, nsor_text *text);
 
 /* Multi-threaded fields-only walk over contiguous shards (CPU baseline). */
+/* Distinct 128-byte lines holding the bytes the chain must inspect,
+ * [off, off + W) per packet (the batch's line floor; bench.py's roofline) */
+uint64_t nsor_line_floor_mt(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n, int linktype, int mode,
+			    int nthreads);
+
 uint64_t nsor_dissect_batch_mt(const uint8_t *frames, const nsd_desc_t *desc, uint32_t n,
 			       int linktype, int mode, nsd_rec *rec, uint64_t *counters,
 			       int nthreads);

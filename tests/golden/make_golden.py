@@ -21,6 +21,8 @@
   shard_counters.json  the oracle's PRINT_NORM counter vector per bench shard
                        (bench.py checks the all-reduced device counters
                        against their sum; --shards-only: these two only)
+  lines.json           the line floor per bench shard (distinct 128-byte lines
+                       of the bytes the chains inspect; --lines-only)
   ip_vectors.npz       tests/ip_vectors.py: IPv4 / IPv6 / ICMPv4 frames and
                        the values the reference's csum.h / ipv4.h / ipv6.h
                        give for them (oracle/_ref/libnsdrefip.so; --ip-only)
@@ -144,6 +146,9 @@ def frame_goldens():
 
 def main():
     T.build_native()
+    if "--lines-only" in sys.argv:
+        line_floor_shards()
+        return
     if "--shards-only" in sys.argv:
         wsum_shards()
         return
@@ -231,6 +236,29 @@ def wsum_shards():
     with open(os.path.join(HERE, "shard_counters.json"), "w") as f:
         json.dump(cnts, f)
 
+
+
+def line_floor_shards():
+    """lines.json: the line floor of each bench shard - the distinct 128-byte
+    lines holding the bytes its chains must inspect ([off, off + W) per
+    packet, nsor_line_floor_mt), the least whole-line HBM reads any schedule
+    can fetch (bench.py reports the measured traffic against it)."""
+    import ctypes
+    L = T.oracle()
+    L.nsor_line_floor_mt.restype = ctypes.c_uint64
+    L.nsor_line_floor_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int]
+    lines = {}
+    n = 1 << 24
+    for key, cfg, shards in (("imix", T.SYN_IMIX, 8), ("ipv6x", T.SYN_IPV6X, 8), ("udp64", T.SYN_UDP64, 8)):
+        for r in range(shards):
+            frames, desc = T.make_batch(cfg, n, lo=r * n)
+            lines[f"{key}:{r * n}:{n}"] = int(L.nsor_line_floor_mt(frames.ctypes.data, desc.ctypes.data, n, 1,
+                                                                   T.PRINT_NORM, 8))
+            del frames, desc
+            print(key, r, lines[f"{key}:{r * n}:{n}"], flush=True)
+    with open(os.path.join(HERE, "lines.json"), "w") as f:
+        json.dump(lines, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -43,6 +43,15 @@ def test_version_and_device_count():
     assert nsd.lib().nsd_device_count() >= 0
 
 
+def test_library_carries_the_tree_source_hash():
+    """The library names the sources it was built from (nsd_build_info's
+    `sources` hash, the Makefile's SRCHASH) and they are this tree's: what
+    a bench line's `library` reports and the test fixture rebuilds on."""
+    info = nsd.lib().nsd_build_info().decode()
+    assert re.search(r"; sources [0-9a-f]{16}$", info), info
+    assert info.endswith(nsd.source_hash()) and nsd.built_source_hash() == nsd.source_hash()
+
+
 def test_device_path_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():

@@ -477,8 +477,9 @@ def test_plain_tiles_partial_and_mixed(mode):
 
 def _imix_tiles(seed=11, n=64 * 48):
     """Ethernet / [one 802.1Q tag] / IPv4 (no options) / TCP, UDP or ICMPv4
-    frames only, so whole tiles take the straight-line IMIX walk
-    (plain4_walk, both schedules): frame lengths 38 .. 1500, total lengths
+    frames only, whole tiles of C3's chains through fast_walk (both
+    schedules; the straight-line plain4 walk of r05 is removed): frame
+    lengths 38 .. 1500, total lengths
     below the header, inside the frame (trimmed) and past it, good and bad
     header checksums, ICMPv4 messages inside the window and past it with
     good and bad sums, odd and even lengths, L4 bodies shorter than their
@@ -542,10 +543,9 @@ def _not_imix(rnd, pkt):
 @pytest.mark.parametrize("align", [1, 2, 16])
 @pytest.mark.parametrize("mode", [T.PRINT_NORM, T.PRINT_LESS])
 def test_imix_tiles(mode, align):
-    """Tiles of IMIX chains only (the straight-line plain4 walk in PRINT_NORM)
-    at odd and even alignments, a partial last tile, and tiles with one
-    frame the path must refuse: records of both forms and counters equal the
-    oracle's, under both schedules."""
+    """Tiles of IMIX chains only at odd and even alignments, a partial last
+    tile, and tiles with one other frame: records of both forms and counters
+    equal the oracle's, under both schedules."""
     import random
     rnd = random.Random(31 + align)
     pkts = _imix_tiles(seed=align, n=64 * 40 + 9)

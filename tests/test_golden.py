@@ -191,6 +191,30 @@ def test_names_on(name, mode):
         assert texts[i] == gold[i], f"formatter packet {i}"
 
 
+def test_line_floor_golden():
+    """lines.json (bench.py's line floor) is the restatement's: shard 0 of C3
+    and C4 recomputed (distinct 128-byte lines of [off, off + W) per packet),
+    and the floor is at least the algorithmic bytes W (a line holds at most
+    128 of them)."""
+    import ctypes
+    L = T.oracle()
+    L.nsor_line_floor_mt.restype = ctypes.c_uint64
+    L.nsor_line_floor_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int]
+    with open(os.path.join(G, "lines.json")) as f:
+        lines = json.load(f)
+    with open(os.path.join(G, "wsum.json")) as f:
+        wsum = json.load(f)
+    n = 1 << 24
+    for key, cfg in (("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):
+        frames, desc = T.make_batch(cfg, n)
+        got = int(L.nsor_line_floor_mt(frames.ctypes.data, desc.ctypes.data, n, 1, T.PRINT_NORM, 8))
+        del frames, desc
+        assert got == lines[f"{key}:0:{n}"], key
+        assert 128 * got >= wsum[f"{key}:0:{n}"], key
+    assert lines[f"udp64:0:{n}"] == n // 2   # 64-byte frames, two to a line
+
+
 def test_prefix_digests():
     """64K-packet prefixes of C2/C3/C4: oracle records + counters + ΣW match
     the committed digests (text digests were taken from nsref)."""

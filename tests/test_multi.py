@@ -103,6 +103,39 @@ def test_bench_line_n_ranks(tmp_path):
     assert bench.golden_counters("imix", 1 << 24, 8) is not None   # the C5 shards are in the table
 
 
+def test_bench_cli_n_ranks():
+    """The launch path the driver's N-GPU run takes, end to end on CPU:
+    `python bench.py --gpus 2` with no launcher -> nsd_dist.spawn_ranks ->
+    torch.distributed.run -> main() in each rank -> nsd_dist.init -> run()
+    (the hidden --engine host switch: gloo and the product's host walk in
+    place of RCCL and the kernels).  Rank 0's line: n_gpus 2, the legs, and
+    the all-reduced counters equal the oracle's over both ranks' shards x
+    the steps."""
+    import json
+    import nsd
+    world, per_rank, steps = 2, 3000, 2
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--engine", "host",
+                        "--packets", str(per_rank), "--steps", str(steps), "--warmup", "1", "--no-pmc"],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    assert r.returncode == 0, r.stderr.decode(errors="replace")[-2000:]
+    lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout.decode()[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and line["config"]["parallelism"] == "dp2" and line["scaling"] == "weak"
+    assert line["counters_total"] == world * per_rank * steps and line["setup_s"] >= 0
+    assert line["bench_wall_s"] > 0
+    assert set(line["legs"]) == {"imix", "ipv6x"}
+    for key, cfg in (("imix", T.SYN_IMIX), ("ipv6x", T.SYN_IPV6X)):
+        leg = line["legs"][key]
+        assert leg["packets"] == world * per_rank and leg["schedule"] == "host walk"
+        frames, desc = T.make_batch(cfg, world * per_rank)
+        _, _, want, _ = T.oracle_records(frames, desc)
+        assert leg["counters"] == nsd.unpack_counters(want * np.uint64(steps)), key
+
+
 def _dev_worker(rank, world, port, key, per_rank, steps, out):
     """One rank of the device branch: both ranks on cuda:0 (one GPU box),
     gloo over CUDA tensors (RCCL refuses two ranks on one device)."""

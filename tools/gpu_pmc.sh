@@ -13,6 +13,7 @@ G[fetch]="FETCH_SIZE"
 G[write]="WRITE_SIZE"
 G[tcc]="TCC_HIT_sum TCC_MISS_sum"
 G[req]="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+G[wreq]="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"
 for g in ${PASSES:-sq1 sq2}; do
   timeout -s KILL 120 rocprofv3 --pmc ${G[$g]} --kernel-trace -d "$O/${CFG}_$g" -o run --output-format csv -- python3 "$R/bench.py" --config ${CFG:-udp64} --steps 3 --warmup 1 --no-cpu --no-e2e --no-replay --no-legs --no-pmc --no-bpf > "$O/${CFG}_$g.log" 2>&1; rc=$?
   echo "pmc $g rc=$rc"; [ $rc = 0 ] || { tail -5 "$O/${CFG}_$g.log"; exit $rc; }
