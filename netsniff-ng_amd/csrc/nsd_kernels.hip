@@ -77,6 +77,9 @@ constexpr int row_of(int W) { return W / 4 + 4; }
 #ifndef NSD_FAST_EXT
 #define NSD_FAST_EXT 1             // the fused kernel's fast walk steps extension headers in its window
 #endif
+#ifndef NSD_WIN_NT
+#define NSD_WIN_NT 1               // the walkers' window loads nontemporal (stage_glds)
+#endif
 #ifndef NSD_RING
 #define NSD_RING 1                 // the fused kernel's compact records through the per-wave record ring (RingSt)
 #endif
@@ -368,7 +371,12 @@ __device__ __forceinline__ void stage_write(uint32_t *wwin, const Chunks<WIN> &c
 // in slot c ^ swz(q) and the lanes reading one window offset spread over
 // the banks (dword j of row q at j ^ (swz(q) << 2)).  No VGPR holds the
 // window on the way.  Chunks wholly past the frame are not loaded (the
-// source masks the bytes past caplen instead).  abase: this lane's aligned
+// source masks the bytes past caplen instead).  The loads are nontemporal
+// (NSD_WIN_NT): a window's lines are read once, and as L2-allocating loads
+// they pushed out the packets' first lines that the late chunk loads had
+// just brought in for the walkers (C4: 308.6 -> 259.4 B/packet read, 40.5M
+// -> 34.0M 128-byte requests per launch against a line floor of 262.9;
+// kernel time unchanged).  abase: this lane's aligned
 // window start in HBM; rem: bytes from there to the frame's aligned end (0:
 // the lane takes no window).
 __device__ __forceinline__ uint32_t swz_of(uint32_t q, int cpp) { return (q >> 1) & (uint32_t)(cpp - 1); }
@@ -390,7 +398,7 @@ __device__ __forceinline__ void stage_glds(uint32_t *wwin, uint64_t abase, uint3
 			const uint64_t a = ((uint64_t)(ahr & 0xFFFFu) << 32 | alo) + 16 * c;
 			__builtin_amdgcn_global_load_lds((const void *)a,
 							 (__attribute__((address_space(3))) void *)(wwin + r * 256), 16, 0,
-							 0);
+							 NSD_WIN_NT ? 2 : 0);
 		}
 	}
 	// the DMA's LDS writes are ordered for this wave's reads by its vmcnt only
@@ -695,11 +703,15 @@ struct Shared {
 	uint8_t tmap[WAVES][64];                    // take(): pending lane of each rank
 };
 
-// The fused kernel's record ring (compact records).  A tile whose packets
-// the fast walk all finishes stores its records at once, right after its
-// fast walk (C3: the same time as r05's records held one tile in registers,
-// HeldSt, which no longer fit beside the ring's code: 11 VGPRs spilled,
-// C3 +28 %).  A tile with deferred packets has its records written
+// The fused kernel's record ring (compact records of walker-heavy batches:
+// a build of its own, dissect_all<MODE, true, true>, which the launcher runs
+// when the schedule sample defers more than a quarter of the packets; the
+// plain build holds a tile's records one tile in registers, HeldSt, which do
+// not fit beside the ring's code: 11 VGPRs spilled, C3 +28 %, and stored
+// right after the fast walk instead C3 ran 4 % slower).  In the ring build
+// a tile whose packets the fast walk all finishes stores its records at
+// once, right after its fast walk.  A tile with deferred packets has its
+// records written
 // twice over: by the fast walk (the packets it finishes) and later by the
 // walkers' sessions (each session's finished packets), often across two
 // tiles.  Stored to HBM as they came, a 128-byte line of records (16
@@ -716,8 +728,10 @@ struct Shared {
 // tile while packets of its old tile are still held by walkers (walked
 // across two more tiles) stores the finished ones at once, and those
 // walkers store theirs directly (the tile has left the ring).  The state is
-// wave-uniform and lives in scalar registers: a round trip to LDS for it
-// before each tile's prefetch loads cost C3 5 %.
+// wave-uniform and lives in scalar registers (a round trip to LDS for it
+// before each tile's prefetch loads cost 5 %).  C4: 23.7 -> 12.2 B/packet
+// written per launch, kernel time within the box's noise (+-1 %: C4's
+// walker steps, not its bytes, set its time).
 constexpr uint32_t RING_NONE = 0xFFFFFFFFu;
 struct RingSt {
 	// (scalars, never an array indexed at run time: that would go to scratch)
@@ -1252,7 +1266,7 @@ __device__ __forceinline__ void prio_level(uint32_t lvl)
 		__builtin_amdgcn_s_setprio(0);
 }
 
-template <int MODE, bool CR>
+template <int MODE, bool CR, bool RING>
 __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict__ frames,
 					   const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 					   void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
@@ -1383,7 +1397,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	hs.ri = hs.pp = 0xFFFFFFFFu;
 	// compact records: the wave's record ring (RecRing), slot rs for the
 	// next tile
-	constexpr bool RG = CR && NSD_RING;
+	constexpr bool RG = CR && RING;
 	RingSt rs;
 	rs.init();
 	// (one more pass after the last tile drains the walkers: the engine is
@@ -1392,7 +1406,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 	const uint32_t share = (ntiles + nw - 1) / nw;
 	uint32_t done = 0, lvl = 0xFFu;
 	for (;;) {
-		if (NSD_PRIO && CR && (prio & 1)) {   // (the 16-byte form's walk state leaves no registers for it)
+		if (NSD_PRIO && CR && prio) {   // (the 16-byte form's walk state leaves no registers for it)
 			const uint32_t l = done < share ? 4u * done / share : 3u;
 			if (l != lvl) {
 				lvl = l;
@@ -1480,7 +1494,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			if (lend)
 				w.flags |= NSD_F_LEAF_END;
 			const uint32_t nd = (uint32_t)__popcll(__ballot(deferred));
-			if (RG && (prio & 2) && nd) {
+			if (RG && nd) {
 				ring_open(sh, rs, base, nd, done, crec_of(w), lend ? w.data : 0u, lane);
 			} else if (CR && !RG) {
 				if (lend)
@@ -1555,7 +1569,7 @@ __device__ __forceinline__ void walk_tiles(Shared &sh, const uint8_t *__restrict
 			base += stride;
 		}
 	}
-	if (NSD_PRIO && CR && (prio & 1))
+	if (NSD_PRIO && CR && prio)
 		__builtin_amdgcn_s_setprio(0);   // the leaf and checksum passes at the neutral level
 	fc.flush(s_cnt, lane);
 	// the pending list held every entry (ask()'s room rule: a packet adds at
@@ -1634,7 +1648,7 @@ __global__ void zero_tiles(uint32_t *__restrict__ gtiles, uint32_t groups)
 		gtiles[32 * i] = 0;
 }
 
-template <int MODE, bool CR>
+template <int MODE, bool CR, bool RING = false>
 __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 	void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
@@ -1654,8 +1668,8 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_all(
 	// this wave's pending list (a wave visits region / WAVES packets)
 	Pending pq{ pend + ((size_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (region / WAVES), region / WAVES, 0,
 		    0 };
-	walk_tiles<MODE, CR>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq, sched,
-			     gtiles, prio);
+	walk_tiles<MODE, CR, RING>(sh, frames, desc, n, start_id, rec, ext, ext_words, ext_used, chunk, sll, pq,
+				   sched, gtiles, prio);
 	if (MODE == PRINT_NORM || MODE == PRINT_LESS)
 		leaf_pass<MODE, CR>(frames, desc, rec, ext, pq);
 	if ((threadIdx.x & 63) == 0)
@@ -2663,9 +2677,15 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 		{ dissect_all<PRINT_NORM, false>, dissect_all<PRINT_LESS, false>, dissect_all<PRINT_HEX, false> },
 		{ dissect_all<PRINT_NORM, true>, dissect_all<PRINT_LESS, true>, dissect_all<PRINT_HEX, true> },
 	};
-	static std::atomic<int> s_occ[2][3];
-	const kfn f = kernels[ci][mi];
-	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)(s_cus * occupancy((const void *)f, s_occ[ci][mi], 4));
+	// compact records of walker-heavy batches: the record ring's build (an
+	// instantiation of its own: beside the ring's code, the records held one
+	// tile in registers spill, and without them C3 runs 4 % slower)
+	static const kfn ring_kernels[2] = { dissect_all<PRINT_NORM, true, true>, dissect_all<PRINT_LESS, true, true> };
+	static std::atomic<int> s_occ[2][3], s_rocc[2];
+	const bool ring = NSD_RING && plan.ring && ci == 1 && mi < 2;
+	const kfn f = ring ? ring_kernels[mi] : kernels[ci][mi];
+	std::atomic<int> &occ_slot = ring ? s_rocc[mi] : s_occ[ci][mi];
+	uint32_t cap_blocks = grid > 0 ? (uint32_t)grid : (uint32_t)(s_cus * occupancy((const void *)f, occ_slot, 4));
 	if (cap_blocks > NSD_MAX_GRID)
 		cap_blocks = NSD_MAX_GRID;
 	const uint32_t blocks = want < cap_blocks ? want : cap_blocks;
@@ -2683,7 +2703,7 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	hipLaunchKernelGGL(f, dim3(blocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec, d_ext,
 			   ext_words, d_ext_used, chunk_for(blocks), (unsigned long long *)d_counters, (uint64_t *)d_ws,
 			   region_for_fused(n, blocks, compact), (const uint32_t *)d_sll, sched, gtiles,
-			   (plan.prio ? 1u : 0u) | (plan.ring ? 2u : 0u));
+			   plan.prio ? 1u : 0u);
 	if (hipGetLastError() != hipSuccess) {
 		if (sched)
 			sched_abort(stream);

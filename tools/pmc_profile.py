@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PACKETS = 1 << 24
 
 
-def counters(cfg, kernels=("dissect_all<0, true>", "dissect_fast<0, true>", "dissect_walk<0, true>")):
+def counters(cfg, kernels=("dissect_all<0, true", "dissect_fast<0, true>", "dissect_walk<0, true>")):
     """Per-launch counter values: each kernel's average over its dispatches,
     summed over the kernels of one launch (dissect_fast + dissect_walk, or
     dissect_all)."""
