@@ -78,7 +78,7 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "round")):
                     if "nsd::dissect_" not in nm or "<0," not in nm:
                         continue
                     kern = nm.split("nsd::")[1].split("<")[0]
-                    form = "true" if "<0, true>" in nm else "false"
+                    form = "true" if ("<0, true>" in nm or "<0, true," in nm) else "false"
                     launches[form].append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), kern))
 
             def steps_of(ks):
