@@ -376,15 +376,14 @@ NSD_HD int sll_next(uint32_t hatype, uint32_t proto, int mode, uint32_t e2)
 // the chain needs the ext form), count it, advance the pkt_buff cursor
 // exactly as the reference parser does, look up the next ops.
 // `info0`: the ops' rule word s.step(w.id), when the caller has read it.
-template <int MODE, class Src, class Sink>
-NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g, uint32_t info0)
+// Record the layer the lane runs (`act`: ops w.id at w.data): the first 6 in
+// the record; more than 6, or a layer past byte 510, forces the ext form
+template <class Sink>
+NSD_HD void record_layer(bool act, WalkOut &w, const Sink &g)
 {
 	const int id = act ? w.id : 0;
 	const uint32_t start = w.data;
 	const uint32_t k = w.n;
-	const uint32_t info = act ? info0 : 0u;
-	// ---- record the layer: the first 6 in the record; more than 6, or a
-	// layer past byte 510, forces the ext form
 	constexpr uint32_t DEEP = NSD_REC_MAX_LAYERS + NSD_LDS_LAYERS;
 	const bool need_now = act && (k >= NSD_REC_MAX_LAYERS || (k >= 1 && start > 510));
 	g.take_deep(act && k == DEEP, w);   // (entry taken unless ext_on)
@@ -402,6 +401,15 @@ NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g, uint32_t
 	if (act && k < NSD_EXT_MAX_LAYERS)
 		g.layer(w, k, id, start);
 	w.n = act ? k + 1 : k;
+}
+
+template <int MODE, class Src, class Sink>
+NSD_HD void gen_step(const Src &s, bool act, WalkOut &w, const Sink &g, uint32_t info0)
+{
+	const int id = act ? w.id : 0;
+	const uint32_t start = w.data;
+	const uint32_t info = act ? info0 : 0u;
+	record_layer(act, w, g);
 
 	// ---- parse.  Every use of the layer's bytes (B0, KD) is gated by the
 	// first pull (pulled), so bytes past the frame, which the device's
