@@ -1725,6 +1725,9 @@ constexpr int FROW = WIN1 / 4;   // fast rows: 16 dwords, 16-byte slots XOR-swiz
 #ifndef NSD_FAST_BPC
 #define NSD_FAST_BPC (NSD_FAST_DEPTH > 1 ? 3 : 0)   // resident fast blocks per CU (0: as many as fit)
 #endif
+#ifndef NSD_SPLIT_TAIL
+#define NSD_SPLIT_TAIL 1           // the fast kernel's blocks walk their own deferrals (no walker launch)
+#endif
 #ifndef NSD_FAST_CSUM_U
 #define NSD_FAST_CSUM_U 8        // interior chunk loads in flight per lane (fast_icmp_pass; 4: C3 split +4 %)
 #endif
@@ -2165,14 +2168,33 @@ __device__ __forceinline__ void fast_icmp_pass(FastShared &sh, const uint8_t *__
 }
 
 template <int MODE, bool CR>
+__device__ __forceinline__ void walk_lists(Shared &sh, uint32_t *s_touch, const uint8_t *__restrict__ frames,
+					   const uint64_t *__restrict__ desc, uint32_t n, void *__restrict__ rec,
+					   uint32_t *__restrict__ ext, uint32_t ext_words, uint32_t *__restrict__ ext_used,
+					   uint32_t chunk, unsigned long long *__restrict__ counters,
+					   const uint4 *__restrict__ lists, uint32_t cap, const uint2 *__restrict__ cnts,
+					   uint32_t nlists, uint32_t nw, uint64_t *__restrict__ pend, uint32_t region);
+
+// The split schedule's fast kernel.  `tail` (NSD_SPLIT_TAIL): a block whose
+// waves deferred packets walks them itself after its tiles (walk_lists over
+// its own four lists, the walker pool's LDS in the same words as the fast
+// rows), so a batch the fast walk finishes takes one launch instead of two
+// (C2: the walker kernel's empty launch cost 4.9 us of 205, at any grid).
+template <int MODE, bool CR>
 __global__ __launch_bounds__(BLOCK, CR ? NSD_FAST_MINW : NSD_FAST_MINW_FULL) void dissect_fast(
 	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n, int start_id,
 	void *__restrict__ rec, unsigned long long *__restrict__ counters, uint4 *__restrict__ lists, uint32_t cap,
 	uint2 *__restrict__ cnts, const uint32_t *__restrict__ sll, uint32_t *__restrict__ side,
-	unsigned long long *__restrict__ sched)
+	unsigned long long *__restrict__ sched, uint32_t *__restrict__ ext, uint32_t ext_words,
+	uint32_t *__restrict__ ext_used, uint32_t chunk, uint64_t *__restrict__ pend, uint32_t region, uint32_t tail)
 {
 	constexpr int SW = 2;
-	__shared__ FastShared sh;
+	union FastLds {
+		FastShared f;
+		Shared w;
+	};
+	__shared__ FastLds su;
+	FastShared &sh = su.f;
 	if (threadIdx.x < 32)
 		sh.ops[threadIdx.x] = 0;
 	block_init(sh.cnt, sh.lay3);
@@ -2196,6 +2218,15 @@ __global__ __launch_bounds__(BLOCK, CR ? NSD_FAST_MINW : NSD_FAST_MINW_FULL) voi
 	block_flush(sh.cnt, counters);
 	if (threadIdx.x < 32 && sh.ops[threadIdx.x])
 		atomicAdd(&counters[NSD_CNT_OPS + threadIdx.x], (unsigned long long)sh.ops[threadIdx.x]);
+	if constexpr (NSD_SPLIT_TAIL && (MODE == PRINT_NORM || MODE == PRINT_LESS)) {
+		// (the barrier also orders the flush's LDS reads before the walker
+		// pool's set-up in the same words)
+		if (__syncthreads_or(tail && ndef != 0)) {
+			__shared__ uint32_t s_touch[64];
+			walk_lists<MODE, CR>(su.w, s_touch, frames, desc, n, rec, ext, ext_words, ext_used, chunk, counters,
+					     lists, cap, cnts, gridDim.x * WAVES, gridDim.x * WAVES, pend, region);
+		}
+	}
 }
 
 // The walker kernel: wave g of the grid takes the fast kernel's lists g,
@@ -2206,28 +2237,19 @@ __global__ __launch_bounds__(BLOCK, CR ? NSD_FAST_MINW : NSD_FAST_MINW_FULL) voi
 // chunks ahead, and while chunk c's walkers run, the first windows of chunk
 // c + 1 (at each packet's cursor) are touched into L2 by 4-byte LDS-DMA loads
 // (no VGPR waits for them): its sessions then stage from L2.
+// The walker pool over the fast kernel's deferral lists: wave gw takes lists
+// gw, gw + nw, ... (nw: the list stride; the fast kernel's own tail passes
+// nlists, so each wave takes its own list only), then the block's leaves and
+// ICMPv4 checksums.  s_touch: the L2 touches' LDS-DMA target (never read).
 template <int MODE, bool CR>
-__global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
-	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n,
-	void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
-	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
-	const uint4 *__restrict__ lists, uint32_t cap, const uint2 *__restrict__ cnts, uint32_t nlists,
-	uint64_t *__restrict__ pend, uint32_t region)
+__device__ __forceinline__ void walk_lists(Shared &sh, uint32_t *s_touch, const uint8_t *__restrict__ frames,
+					   const uint64_t *__restrict__ desc, uint32_t n, void *__restrict__ rec,
+					   uint32_t *__restrict__ ext, uint32_t ext_words, uint32_t *__restrict__ ext_used,
+					   uint32_t chunk, unsigned long long *__restrict__ counters,
+					   const uint4 *__restrict__ lists, uint32_t cap, const uint2 *__restrict__ cnts,
+					   uint32_t nlists, uint32_t nw, uint64_t *__restrict__ pend, uint32_t region)
 {
 	constexpr int SW = 2;
-	__shared__ Shared sh;
-	__shared__ uint32_t s_touch[64];   // the L2 touches' LDS-DMA target (never read)
-	{
-		// nothing deferred to this block's waves (the common case of traffic
-		// the fast walk finishes): leave before any set-up
-		const uint32_t nw = gridDim.x * WAVES;
-		bool any = false;
-		for (uint32_t L = blockIdx.x * WAVES + (threadIdx.x % WAVES) + (threadIdx.x / WAVES) * nw; L < nlists;
-		     L += (BLOCK / WAVES) * nw)
-			any = any || cnts[L].x != 0;
-		if (!__syncthreads_or(any))
-			return;
-	}
 	if (threadIdx.x < 64)
 		sh.step[threadIdx.x] = threadIdx.x < 32 ? c_step[threadIdx.x] : c_lay2h.e[threadIdx.x - 32];
 	if (threadIdx.x < 32)
@@ -2236,7 +2258,7 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
 		sh.wc[threadIdx.x >> 1][threadIdx.x & 1] = 0;
 	block_init(sh.cnt, sh.lay3);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-	const uint32_t gw = blockIdx.x * WAVES + wv, nw = gridDim.x * WAVES;
+	const uint32_t gw = blockIdx.x * WAVES + wv;
 	Pending pq{ pend + (size_t)gw * (region / WAVES), region / WAVES, 0, 0 };
 	const bool side = CR && ext_words >= n;
 	const GenSink<CR> g{ ext, ext_words, ext_used, chunk, &sh.wc[wv][0], sh.ops, &sh.lay[wv][0],
@@ -2340,6 +2362,31 @@ __global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
 	block_flush(sh.cnt, counters);
 	if (threadIdx.x < 32 && sh.ops[threadIdx.x])
 		atomicAdd(&counters[NSD_CNT_OPS + threadIdx.x], (unsigned long long)sh.ops[threadIdx.x]);
+}
+
+template <int MODE, bool CR>
+__global__ __launch_bounds__(BLOCK, NSD_MINW) void dissect_walk(
+	const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint32_t n,
+	void *__restrict__ rec, uint32_t *__restrict__ ext, uint32_t ext_words,
+	uint32_t *__restrict__ ext_used, uint32_t chunk, unsigned long long *__restrict__ counters,
+	const uint4 *__restrict__ lists, uint32_t cap, const uint2 *__restrict__ cnts, uint32_t nlists,
+	uint64_t *__restrict__ pend, uint32_t region)
+{
+	__shared__ Shared sh;
+	__shared__ uint32_t s_touch[64];
+	{
+		// nothing deferred to this block's waves (the common case of traffic
+		// the fast walk finishes): leave before any set-up
+		const uint32_t nw = gridDim.x * WAVES;
+		bool any = false;
+		for (uint32_t L = blockIdx.x * WAVES + (threadIdx.x % WAVES) + (threadIdx.x / WAVES) * nw; L < nlists;
+		     L += (BLOCK / WAVES) * nw)
+			any = any || cnts[L].x != 0;
+		if (!__syncthreads_or(any))
+			return;
+	}
+	walk_lists<MODE, CR>(sh, s_touch, frames, desc, n, rec, ext, ext_words, ext_used, chunk, counters, lists, cap,
+			     cnts, nlists, gridDim.x * WAVES, pend, region);
 }
 
 } // namespace nsd
@@ -2721,7 +2768,8 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	return 0;
 	}
 	typedef void (*ffn)(const uint8_t *, const uint64_t *, uint32_t, int, void *, unsigned long long *, uint4 *,
-			    uint32_t, uint2 *, const uint32_t *, uint32_t *, unsigned long long *);
+			    uint32_t, uint2 *, const uint32_t *, uint32_t *, unsigned long long *, uint32_t *, uint32_t,
+			    uint32_t *, uint32_t, uint64_t *, uint32_t, uint32_t);
 	typedef void (*wfn)(const uint8_t *, const uint64_t *, uint32_t, void *, uint32_t *, uint32_t, uint32_t *,
 			    uint32_t, unsigned long long *, const uint4 *, uint32_t, const uint2 *, uint32_t, uint64_t *,
 			    uint32_t);
@@ -2755,15 +2803,22 @@ extern "C" int nsd_launch_dissect_rec(const uint8_t *d_frames, const uint64_t *d
 	uint64_t *pend = (uint64_t *)((uint8_t *)cnts + align256((size_t)nlists * 8));
 	// compact records: the pool's side words (when it has them), for leaf ends
 	uint32_t *side = compact && d_ext && ext_words >= n ? d_ext : nullptr;
+	// NSD_SPLIT_TAIL: each fast block walks its own deferrals, one list per
+	// wave (`region` = cap slots of walker pending entries per wave)
+	const bool tail = NSD_SPLIT_TAIL && mi != 2;
 	hipLaunchKernelGGL(fast[ci][mi], dim3(fblocks), dim3(BLOCK), 0, stream, d_frames, d_desc, n, start_id, d_rec,
-			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll, side, sched);
+			   (unsigned long long *)d_counters, lists, cap, cnts, (const uint32_t *)d_sll, side, sched, d_ext,
+			   ext_words, d_ext_used, chunk_for(fblocks), pend, cap * WAVES, tail ? 1u : 0u);
 	if (hipGetLastError() != hipSuccess) {
 		if (sched)
 			sched_abort(stream);
 		return -2;
 	}
-	if (mi == 2)
-		return 0;   // no chains: nothing deferred
+	if (mi == 2 || tail) {
+		if (sched && tail)
+			sched_sampled(sched, d_counters, stream);
+		return 0;   // no chains: nothing deferred; or the fast blocks walked their own
+	}
 	uint32_t wcap = grid > 0 ? (uint32_t)grid
 				 : (uint32_t)(s_cus * occupancy((const void *)walk[ci][mi], s_wocc[ci][mi], 4));
 #ifdef NSD_WALK_GRID_CAP
