@@ -17,7 +17,7 @@ import subprocess
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "_ZN3nsd11dissect_allILi0ELb1EEEv"   # (prefix of the mangled name)
+KERNEL = os.environ.get("ISA_KERNEL", "_ZN3nsd11dissect_allILi0ELb1ELb1EEEv")   # (prefix of the mangled name: the ring build)
 
 
 def classify(op):
