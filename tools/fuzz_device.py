@@ -2,7 +2,8 @@
 several seeds, modes and alignments, both record forms (16-byte records
 through the host batch entry, compact records through the device-resident
 entry); prints mismatch counts.  GPU box tool:
-  python tools/fuzz_device.py [n] [seeds] [split|fused]"""
+  python tools/fuzz_device.py [n] [seeds] [split|fused] [ring|noring]
+(ring / noring: the fused kernel's record ring forced on / off)"""
 import os
 import sys
 
@@ -20,6 +21,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 200000
 seeds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 if len(sys.argv) > 3:   # split / fused (default: the adaptive choice)
     nsd.set_schedule({"split": nsd.SCHED_SPLIT, "fused": nsd.SCHED_FUSED}[sys.argv[3]])
+if len(sys.argv) > 4:
+    nsd.set_record_ring({"ring": nsd.RING_ON, "noring": nsd.RING_OFF}[sys.argv[4]])
 fails = 0
 for seed in range(seeds):
     for mode, align in ((T.PRINT_NORM, 16), (T.PRINT_LESS, 16), (T.PRINT_NORM, 2)):
