@@ -43,6 +43,20 @@ def test_version_and_device_count():
     assert nsd.lib().nsd_device_count() >= 0
 
 
+def test_record_ring_knob():
+    """nsd_set_record_ring: 0 adaptive / 1 on / 2 off, returns the previous
+    setting, refuses anything else (NSD_ERR_ARG)."""
+    prev = nsd.set_record_ring(nsd.RING_OFF)
+    try:
+        assert nsd.set_record_ring(nsd.RING_ON) == nsd.RING_OFF
+        assert nsd.set_record_ring(nsd.RING_ADAPTIVE) == nsd.RING_ON
+        for bad in (-1, 3):
+            with pytest.raises(ValueError):
+                nsd.set_record_ring(bad)
+    finally:
+        nsd.set_record_ring(prev)
+
+
 def test_library_carries_the_tree_source_hash():
     """The library names the sources it was built from (nsd_build_info's
     `sources` hash, the Makefile's SRCHASH) and they are this tree's: what
